@@ -1,0 +1,432 @@
+"""hbbft_amd -- MI355X-native Reliable-Broadcast data path for hbbft.
+
+Python host-side mirror of the reference's `Coding` / `MerkleTree` / `Proof`
+surface (/root/reference/src/broadcast/broadcast.rs:639-694,
+src/broadcast/merkle.rs) over the C ABI in include/hbrbc.h, plus thin
+wrappers of the batched device entry points that take torch tensors.
+
+Every computation runs in hbbft_amd/libhbrbc.so (HIP kernels for gfx950).
+There is no CPU fallback: importing works anywhere, but the first call that
+needs the library raises `HbrbcUnavailable` when it is not built or no GPU is
+visible.
+"""
+import ctypes
+import os
+
+__all__ = [
+    "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
+    "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhbrbc.so")
+
+STATUS_NAMES = {
+    0: "Ok", 1: "TooFewShards", 2: "TooManyShards", 3: "TooFewDataShards",
+    4: "TooManyDataShards", 5: "TooFewParityShards", 6: "TooManyParityShards",
+    7: "TooFewBufferShards", 8: "TooManyBufferShards", 9: "IncorrectShardSize",
+    10: "TooFewShardsPresent", 11: "EmptyShard", 12: "InvalidShardFlags", 13: "InvalidIndex",
+    64: "SingularMatrix", 65: "RootMismatch", 66: "NoPayloadLen",
+    100: "InvalidArgument", 101: "DeviceError", 102: "NoDevice",
+}
+STAGES = ["frame", "encode", "leaf_hash", "tree_levels", "proofs", "validate",
+          "decode_matrix", "reconstruct", "unframe"]
+
+
+class HbrbcUnavailable(RuntimeError):
+    """libhbrbc.so is missing or no HIP device is visible (no fallback exists)."""
+
+
+class RseError(Exception):
+    """A `reed_solomon_erasure::Error` (or library error) returned by the ABI."""
+
+    def __init__(self, code, msg=""):
+        self.code = code
+        self.name = STATUS_NAMES.get(code, "Status%d" % code)
+        super().__init__("%s%s" % (self.name, (": " + msg) if msg else ""))
+
+
+_lib = None
+_P = ctypes.c_void_p
+_S = ctypes.c_size_t
+
+
+def lib():
+    """Load libhbrbc.so (raises HbrbcUnavailable if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HbrbcUnavailable("%s not built (run __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "hbrbc_last_error": (ctypes.c_char_p, []),
+        "hbrbc_version": (ctypes.c_char_p, []),
+        "hbrbc_coding_new": (ctypes.c_int, [_S, _S, ctypes.c_int, ctypes.POINTER(_P)]),
+        "hbrbc_coding_free": (None, [_P]),
+        "hbrbc_data_shard_count": (_S, [_P]),
+        "hbrbc_parity_shard_count": (_S, [_P]),
+        "hbrbc_encoding_matrix": (ctypes.c_int, [_P, _P]),
+        "hbrbc_stream": (_P, [_P]),
+        "hbrbc_encode": (ctypes.c_int, [_P, _P, _P, _S]),
+        "hbrbc_reconstruct": (ctypes.c_int, [_P, _P, _P, _P, _S]),
+        "hbrbc_merkle_node_count": (_S, [_S]),
+        "hbrbc_merkle_max_proof_len": (_S, [_S]),
+        "hbrbc_merkle_build": (ctypes.c_int, [_P, _P, _S, _P]),
+        "hbrbc_merkle_proof": (ctypes.c_int, [_P, _S, _S, _P, ctypes.POINTER(_S)]),
+        "hbrbc_proof_validate": (ctypes.c_int, [_P, _S, _S, _P, _S, _P, _S,
+                                                ctypes.POINTER(ctypes.c_int)]),
+        "hbrbc_shard_len": (_S, [_S, _S]),
+        "hbrbc_frame_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _S, _S, _P]),
+        "hbrbc_encode_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P]),
+        "hbrbc_merkle_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P, _S, _P]),
+        "hbrbc_proofs_batch": (ctypes.c_int, [_P, _P, _S, _S, _P, _P, _P]),
+        "hbrbc_validate_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P, _P, _P, _P, _S, _S,
+                                                _S, _P, _P]),
+        "hbrbc_reconstruct_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _P, _P]),
+        "hbrbc_decode_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _P, _S, _P, _S, _P, _S,
+                                              _P, _P, _P]),
+        "hbrbc_reserve": (ctypes.c_int, [_P, _S]),
+        "hbrbc_profile_enable": (ctypes.c_int, [_P, ctypes.c_int]),
+        "hbrbc_profile_reset": (ctypes.c_int, [_P]),
+        "hbrbc_profile_read": (ctypes.c_int, [_P, _P, _P]),
+        "hbrbc_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(code):
+    if code != 0:
+        raise RseError(code, lib().hbrbc_last_error().decode(errors="replace"))
+
+
+def shard_len(payload_len, data_shards):
+    """broadcast.rs:182 -- ceil((len + 4) / data_shards)."""
+    return (payload_len + 4 + data_shards - 1) // data_shards
+
+
+def merkle_node_count(n):
+    total, sz = 0, n
+    while True:
+        total += sz
+        if sz <= 1:
+            return total
+        sz = (sz + 1) // 2
+
+
+def max_proof_len(n):
+    d, sz = 0, n
+    while sz > 1:
+        d += 1
+        sz = (sz + 1) // 2
+    return d
+
+
+def _as_buffer(b):
+    """A writable contiguous uint8 buffer for bytes-like / numpy input."""
+    import numpy as np
+    if isinstance(b, np.ndarray):
+        assert b.dtype == np.uint8 and b.flags.c_contiguous
+        return b
+    if isinstance(b, bytearray):
+        return np.frombuffer(b, dtype=np.uint8)
+    return np.frombuffer(bytearray(b), dtype=np.uint8)
+
+
+def _addr(a):
+    return a.ctypes.data if a.size else 0
+
+
+# --------------------------------------------------------------------------
+# Mirror of `Coding` (broadcast.rs:639-694)
+# --------------------------------------------------------------------------
+class Coding:
+    """`Coding::new(data_shard_num, parity_shard_num)`; parity 0 = Trivial."""
+
+    def __init__(self, data_shard_num, parity_shard_num, device=-1):
+        h = _P()
+        _check(lib().hbrbc_coding_new(data_shard_num, parity_shard_num, device, ctypes.byref(h)))
+        self._h = h
+
+    @classmethod
+    def for_validators(cls, n, device=-1):
+        """Broadcast::new (broadcast.rs:98-101): f = (n-1)/3, parity 2f, data n-2f."""
+        f = (n - 1) // 3
+        return cls(n - 2 * f, 2 * f, device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().hbrbc_coding_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def data_shard_count(self):
+        return lib().hbrbc_data_shard_count(self._h)
+
+    def parity_shard_count(self):
+        return lib().hbrbc_parity_shard_count(self._h)
+
+    def encoding_matrix(self):
+        import numpy as np
+        k, m = self.data_shard_count(), self.parity_shard_count()
+        out = np.zeros((k + m, k), np.uint8)
+        _check(lib().hbrbc_encoding_matrix(self._h, out.ctypes.data))
+        return out
+
+    def encode(self, shards):
+        """`Coding::encode(&mut [&mut [u8]])`: parity shards overwritten in place."""
+        import numpy as np
+        bufs = [_as_buffer(s) for s in shards]
+        for s, b in zip(shards, bufs):
+            if not isinstance(s, (np.ndarray, bytearray)):
+                raise TypeError("encode needs mutable shards (bytearray / np.uint8)")
+        ptrs = (ctypes.c_void_p * max(len(bufs), 1))(*[_addr(b) for b in bufs])
+        lens = (ctypes.c_size_t * max(len(bufs), 1))(*[b.size for b in bufs])
+        _check(lib().hbrbc_encode(self._h, ptrs, lens, len(bufs)))
+
+    def reconstruct_shards(self, shards):
+        """`Coding::reconstruct_shards(&mut [Option<Box<[u8]>>])`: None entries are
+        replaced by the rebuilt shard (bytes) in place."""
+        import numpy as np
+        present = [s is not None for s in shards]
+        lens = [len(s) if s is not None else 0 for s in shards]
+        L = max([l for l, p in zip(lens, present) if p], default=0)
+        bufs = [np.frombuffer(bytes(s), np.uint8).copy() if s is not None else
+                np.zeros(max(L, 1), np.uint8) for s in shards]
+        ptrs = (ctypes.c_void_p * max(len(bufs), 1))(*[_addr(b) for b in bufs])
+        lns = (ctypes.c_size_t * max(len(bufs), 1))(*lens)
+        pres = (ctypes.c_uint8 * max(len(bufs), 1))(*[1 if p else 0 for p in present])
+        _check(lib().hbrbc_reconstruct(self._h, ptrs, lns, pres, len(bufs)))
+        for i, p in enumerate(present):
+            if not p:
+                shards[i] = bufs[i][:L].tobytes()
+
+
+# --------------------------------------------------------------------------
+# Mirror of `MerkleTree` / `Proof` (merkle.rs)
+# --------------------------------------------------------------------------
+class Proof:
+    """`Proof<T>` (merkle.rs:72-78); field order value, index, digests, root_hash."""
+
+    __slots__ = ("_value", "_index", "_digests", "_root")
+
+    def __init__(self, value, index, digests, root_hash):
+        self._value = bytes(value)
+        self._index = int(index)
+        self._digests = [bytes(d) for d in digests]
+        self._root = bytes(root_hash)
+
+    def validate(self, n):
+        """`Proof::validate(n)` (merkle.rs:83-103), on the GPU."""
+        v = _as_buffer(self._value) if self._value else None
+        dig = b"".join(self._digests)
+        d = _as_buffer(dig) if dig else None
+        r = _as_buffer(self._root)
+        ok = ctypes.c_int(0)
+        _check(lib().hbrbc_proof_validate(_addr(v) if v is not None else 0, len(self._value),
+                                          self._index, _addr(d) if d is not None else 0,
+                                          len(self._digests), _addr(r), n, ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def index(self):
+        return self._index
+
+    def root_hash(self):
+        return self._root
+
+    def value(self):
+        return self._value
+
+    def digests(self):
+        return list(self._digests)
+
+    def into_value(self):
+        return self._value
+
+    def __eq__(self, other):
+        return (isinstance(other, Proof) and self._value == other._value and
+                self._index == other._index and self._digests == other._digests and
+                self._root == other._root)
+
+    def __repr__(self):
+        return "Proof(index=%d, root=%s, %d digests)" % (self._index, self._root.hex()[:10],
+                                                         len(self._digests))
+
+
+class MerkleTree:
+    """`MerkleTree<T>` (merkle.rs:12-69) built on the GPU."""
+
+    def __init__(self, values, nodes):
+        self._values = values
+        self._nodes = nodes  # numpy [node_count, 32]
+
+    @classmethod
+    def from_vec(cls, values):
+        import numpy as np
+        values = [bytes(v) for v in values]
+        n = len(values)
+        if n == 0:
+            raise RseError(100, "MerkleTree::from_vec of an empty vector panics in the reference")
+        bufs = [np.frombuffer(v, np.uint8) if v else np.zeros(1, np.uint8) for v in values]
+        ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * n)(*[len(v) for v in values])
+        nodes = np.zeros((merkle_node_count(n), 32), np.uint8)
+        _check(lib().hbrbc_merkle_build(ptrs, lens, n, nodes.ctypes.data))
+        return cls(values, nodes)
+
+    def proof(self, index):
+        """`MerkleTree::proof(index)` -> Proof or None."""
+        import numpy as np
+        n = len(self._values)
+        dig = np.zeros((max(max_proof_len(n), 1), 32), np.uint8)
+        nd = ctypes.c_size_t(0)
+        st = lib().hbrbc_merkle_proof(self._nodes.ctypes.data, n, index, dig.ctypes.data,
+                                      ctypes.byref(nd))
+        if st == 13:
+            return None
+        _check(st)
+        return Proof(self._values[index], index, [dig[i].tobytes() for i in range(nd.value)],
+                     self.root_hash())
+
+    def root_hash(self):
+        return self._nodes[-1].tobytes()
+
+    def values(self):
+        return list(self._values)
+
+    def into_values(self):
+        return self._values
+
+    def levels(self):
+        """Leaf digests and every level above them (merkle.rs:13)."""
+        out, off, sz = [], 0, len(self._values)
+        while True:
+            out.append([self._nodes[off + i].tobytes() for i in range(sz)])
+            if sz <= 1:
+                return out
+            off += sz
+            sz = (sz + 1) // 2
+
+
+# --------------------------------------------------------------------------
+# Batched device path over torch CUDA tensors
+# --------------------------------------------------------------------------
+def _ptr(t):
+    return t.data_ptr() if t is not None else 0
+
+
+class RbcBatch:
+    """Batched broadcast data path for `count` instances of one (N, f) on one
+    GPU.  Owns nothing but the `Coding` context; every buffer is a torch tensor
+    on the context's device.  Calls are asynchronous on `stream` (a
+    torch.cuda.Stream; default: torch's current stream)."""
+
+    def __init__(self, n, f=None, device=0):
+        import torch
+        if not torch.cuda.is_available():
+            raise HbrbcUnavailable("no GPU visible: the RBC path has no CPU fallback")
+        self.n = n
+        self.f = (n - 1) // 3 if f is None else f
+        self.m = 2 * self.f
+        self.k = n - self.m
+        self.device = torch.device("cuda", device)
+        with torch.cuda.device(self.device):
+            self.coding = Coding(self.k, self.m, device)
+        self.node_count = merkle_node_count(n)
+        self.dslots = max_proof_len(n)
+
+    # -- layout helpers -----------------------------------------------------
+    @staticmethod
+    def stride_for(S):
+        return (S + 15) // 16 * 16
+
+    def alloc_slab(self, count, S):
+        import torch
+        stride = self.stride_for(S)
+        return torch.empty((count, self.n, stride), dtype=torch.uint8, device=self.device)
+
+    def alloc_nodes(self, count):
+        import torch
+        return torch.empty((count, self.node_count, 32), dtype=torch.uint8, device=self.device)
+
+    def _stream(self, stream):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(s.cuda_stream)
+
+    # -- entry points ----------------------------------------------------------
+    def frame(self, payloads, plen, slab, stream=None):
+        count = slab.shape[0]
+        S = shard_len(plen, self.k)
+        _check(lib().hbrbc_frame_batch(self.coding.handle, _ptr(payloads), payloads.stride(0),
+                                       plen, count, _ptr(slab), S, slab.stride(1),
+                                       slab.stride(0), self._stream(stream)))
+
+    def encode(self, slab, S, stream=None):
+        _check(lib().hbrbc_encode_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
+                                        slab.stride(0), slab.shape[0], self._stream(stream)))
+
+    def merkle(self, slab, S, nodes, stream=None):
+        _check(lib().hbrbc_merkle_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
+                                        slab.stride(0), slab.shape[0], _ptr(nodes),
+                                        nodes.stride(0), self._stream(stream)))
+
+    def proofs(self, nodes, digests, ndig, stream=None):
+        """digests: uint8 [count, n, max(dslots,1), 32]; ndig: uint8 [count, n]."""
+        _check(lib().hbrbc_proofs_batch(self.coding.handle, _ptr(nodes), nodes.stride(0),
+                                        nodes.shape[0], _ptr(digests), _ptr(ndig),
+                                        self._stream(stream)))
+
+    def validate(self, slab, S, digests, ndig, nodes, ok, indices=None, stream=None):
+        """Validate all n proofs of every instance against its own root."""
+        count = slab.shape[0]
+        root = nodes[:, -1, :]
+        _check(lib().hbrbc_validate_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
+                                          slab.stride(0), self.n, _ptr(indices), _ptr(digests),
+                                          _ptr(ndig), _ptr(root), nodes.stride(0), self.n,
+                                          count, _ptr(ok), self._stream(stream)))
+
+    def reconstruct(self, slab, S, present, status, stream=None):
+        _check(lib().hbrbc_reconstruct_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
+                                             slab.stride(0), _ptr(present), slab.shape[0],
+                                             _ptr(status), self._stream(stream)))
+
+    def decode(self, slab, S, present, roots, nodes, payload_out, plen_out, status,
+               stream=None):
+        """roots: uint8 [count, >=32] (row stride multiple of 16)."""
+        _check(lib().hbrbc_decode_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
+                                        slab.stride(0), _ptr(present), slab.shape[0],
+                                        _ptr(roots), roots.stride(0), _ptr(nodes),
+                                        nodes.stride(0), _ptr(payload_out),
+                                        payload_out.stride(0), _ptr(plen_out), _ptr(status),
+                                        self._stream(stream)))
+
+    def reserve(self, count):
+        _check(lib().hbrbc_reserve(self.coding.handle, count))
+
+    # -- profiling ---------------------------------------------------------
+    def profile(self, enable=True):
+        _check(lib().hbrbc_profile_enable(self.coding.handle, 1 if enable else 0))
+
+    def profile_reset(self):
+        _check(lib().hbrbc_profile_reset(self.coding.handle))
+
+    def profile_read(self):
+        ms = (ctypes.c_double * len(STAGES))()
+        cnt = (ctypes.c_uint64 * len(STAGES))()
+        _check(lib().hbrbc_profile_read(self.coding.handle, ms, cnt))
+        return {STAGES[i]: (ms[i], cnt[i]) for i in range(len(STAGES))}

@@ -1,0 +1,217 @@
+/*
+ * hbrbc.h -- C ABI of the MI355X Reliable-Broadcast data path (libhbrbc.so).
+ *
+ * Drop-in boundary for hbbft's `broadcast` data work (reference:
+ * yangl1996/hbbft, /root/reference).  The reference has no FFI of its own:
+ * its seam is the private enum `Coding` (src/broadcast/broadcast.rs:639-694)
+ * and the crate-private module `merkle` (src/broadcast/merkle.rs, exported at
+ * src/broadcast/mod.rs:224).  Every entry point below names the reference
+ * item it replaces.  INTEGRATION.md shows the Rust `extern "C"` binding that
+ * `Coding`/`MerkleTree`/`Proof` delegate to.
+ *
+ * Two layers:
+ *  1. Per-call shims on HOST memory with exactly the reference semantics
+ *     (same argument meaning, same rse::Error outcomes).  They stage through
+ *     the device and run the same HIP kernels as the batched layer.
+ *  2. Batched entry points on DEVICE memory for thousands of independent
+ *     broadcast instances per call (the hot path).  All are asynchronous on
+ *     the given stream (a hipStream_t; NULL = the context's own stream) and
+ *     never allocate, free or synchronise unless documented.
+ *
+ * Batched layout ("shard slab"): instance `i`, shard `j`, byte `b` lives at
+ *   shards + i*inst_stride + j*shard_stride + b,
+ * 0 <= b < shard_len.  Requirements: shard_stride % 16 == 0,
+ * shard_stride >= shard_len, inst_stride % 16 == 0,
+ * inst_stride >= n_shards*shard_stride, base 16-byte aligned.  Bytes in
+ * [shard_len, round_up(shard_len,16)) of a row are padding: the coding
+ * kernels read and write them, hashing never covers them.
+ *
+ * Merkle node slab: instance `i` owns `hbrbc_merkle_node_count(n)` 32-byte
+ * nodes at nodes + i*node_inst_stride: level 0 (the n leaf digests), level 1
+ * (ceil(n/2)), ..., the root last.  This is `MerkleTree::levels` plus
+ * `root_hash` of merkle.rs:12-16 flattened.
+ *
+ * Errors: every function returns an `int` status.  No exception and no
+ * abort crosses this ABI.  Ownership: the caller owns every buffer passed in.
+ */
+#ifndef HBRBC_H
+#define HBRBC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+/* 1..13 mirror reed_solomon_erasure::Error (4.0.x) in declaration order;  */
+/* hbbft maps all of them to `Error::InvalidNodeCount` at construction      */
+/* (broadcast.rs:101) and to `FaultKind::BroadcastDecoding` on reconstruct  */
+/* (broadcast.rs:551-557, 569).                                             */
+enum hbrbc_status {
+    HBRBC_OK = 0,
+    HBRBC_E_TOO_FEW_SHARDS = 1,
+    HBRBC_E_TOO_MANY_SHARDS = 2,
+    HBRBC_E_TOO_FEW_DATA_SHARDS = 3,
+    HBRBC_E_TOO_MANY_DATA_SHARDS = 4,
+    HBRBC_E_TOO_FEW_PARITY_SHARDS = 5,
+    HBRBC_E_TOO_MANY_PARITY_SHARDS = 6,
+    HBRBC_E_TOO_FEW_BUFFER_SHARDS = 7,
+    HBRBC_E_TOO_MANY_BUFFER_SHARDS = 8,
+    HBRBC_E_INCORRECT_SHARD_SIZE = 9,
+    HBRBC_E_TOO_FEW_SHARDS_PRESENT = 10,
+    HBRBC_E_EMPTY_SHARD = 11,
+    HBRBC_E_INVALID_SHARD_FLAGS = 12,
+    HBRBC_E_INVALID_INDEX = 13,
+    /* decode outcomes of decode_from_shards (broadcast.rs:563-601) */
+    HBRBC_E_SINGULAR_MATRIX = 64,
+    HBRBC_E_ROOT_MISMATCH = 65,   /* mtree.root_hash() != root_hash (583-585) */
+    HBRBC_E_NO_PAYLOAD_LEN = 66,  /* fewer than 4 data bytes (592-597)        */
+    /* library errors */
+    HBRBC_E_INVALID_ARG = 100,
+    HBRBC_E_DEVICE = 101,         /* a HIP call failed: see hbrbc_last_error() */
+    HBRBC_E_NO_DEVICE = 102
+};
+
+typedef struct hbrbc_ctx hbrbc_ctx;
+
+/* Message of the last failing call on this thread (static storage). */
+const char *hbrbc_last_error(void);
+/* Library version string ("hbrbc <semver> gfx950"). */
+const char *hbrbc_version(void);
+
+/* ---- context = one `Coding` (broadcast.rs:639-655) --------------------- */
+/* Replaces `Coding::new(data_shard_num, parity_shard_num)`
+ * (broadcast.rs:648-655) -> rse `ReedSolomon::new` + `build_matrix`.
+ * parity == 0 selects `Coding::Trivial`.  Errors: TOO_FEW_DATA_SHARDS
+ * (data == 0), TOO_MANY_SHARDS (data + parity > 256), NO_DEVICE, DEVICE.
+ * `device` < 0 uses the calling thread's current HIP device. */
+int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc_ctx **out);
+void hbrbc_coding_free(hbrbc_ctx *ctx);
+/* `Coding::data_shard_count` / `parity_shard_count` (broadcast.rs:658-671). */
+size_t hbrbc_data_shard_count(const hbrbc_ctx *ctx);
+size_t hbrbc_parity_shard_count(const hbrbc_ctx *ctx);
+/* The (data+parity) x data encoding matrix, row-major (rse `build_matrix`). */
+int hbrbc_encoding_matrix(const hbrbc_ctx *ctx, uint8_t *out);
+/* The context's own stream (a hipStream_t). */
+void *hbrbc_stream(const hbrbc_ctx *ctx);
+
+/* ---- layer 1: per-call shims, host memory, synchronous ------------------ */
+/* `Coding::encode(&mut [&mut [u8]])` (broadcast.rs:674-679, called at 193):
+ * shards[0..data) in, shards[data..n) overwritten with parity. */
+int hbrbc_encode(hbrbc_ctx *ctx, uint8_t *const *shards, const size_t *lens, size_t n_shards);
+/* `Coding::reconstruct_shards(&mut [Option<Box<[u8]>>])` (broadcast.rs:682-693,
+ * called at 569).  present[i] != 0 marks Some(shard); absent slots must point
+ * at writable buffers of the common shard length and are filled (rse
+ * allocates them zeroed, then writes every byte). */
+int hbrbc_reconstruct(hbrbc_ctx *ctx, uint8_t *const *shards, const size_t *lens,
+                      const uint8_t *present, size_t n_shards);
+
+/* Number of nodes in the flattened tree over n leaves (levels + root). */
+size_t hbrbc_merkle_node_count(size_t n);
+/* Depth bound: the largest digest count of any proof over n leaves. */
+size_t hbrbc_merkle_max_proof_len(size_t n);
+/* `MerkleTree::from_vec(Vec<T>)` (merkle.rs:20-33): leaf i = SHA3-256 of
+ * values[i][0..lens[i]); nodes_out receives node_count(n)*32 bytes, the
+ * root last.  Runs on the default device. */
+int hbrbc_merkle_build(const uint8_t *const *values, const size_t *lens, size_t n,
+                       uint8_t *nodes_out);
+/* `MerkleTree::proof(index)` (merkle.rs:36-53): returns HBRBC_OK and fills
+ * digests_out (32*ndig bytes, at most max_proof_len(n) digests), or
+ * HBRBC_E_INVALID_INDEX for index >= n (`None`).  Pure data movement. */
+int hbrbc_merkle_proof(const uint8_t *nodes, size_t n, size_t index, uint8_t *digests_out,
+                       size_t *ndig_out);
+/* `Proof::validate(n)` (merkle.rs:83-103): *valid_out = 1 iff the digests
+ * form a branch from SHA3(value) at `index` to `root` in a tree of n leaves
+ * (too few or too many digests -> 0). */
+int hbrbc_proof_validate(const uint8_t *value, size_t len, size_t index, const uint8_t *digests,
+                         size_t ndig, const uint8_t root[32], size_t n, int *valid_out);
+
+/* ---- layer 2: batched, device memory, asynchronous on `stream` ---------- */
+/* send_shards framing (broadcast.rs:174-189): payload p of instance i (bytes
+ * payloads[i*payload_stride .. +payload_len)) -> data shards 0..data-1 of
+ * the slab hold BE32(payload_len) ++ payload ++ zeros; padding zeroed.
+ * payload_stride % 4 == 0 and >= round_up(payload_len, 4); shard_len must
+ * equal hbrbc_shard_len(payload_len, data). */
+size_t hbrbc_shard_len(size_t payload_len, size_t data_shards);
+int hbrbc_frame_batch(hbrbc_ctx *ctx, const uint8_t *payloads, size_t payload_stride,
+                      size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
+                      size_t shard_stride, size_t inst_stride, void *stream);
+/* Coding::encode over `count` instances (broadcast.rs:193): parity rows
+ * data..n-1 of every instance written in place. */
+int hbrbc_encode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                       size_t inst_stride, size_t count, void *stream);
+/* MerkleTree::from_vec over the n = data+parity shards of every instance
+ * (broadcast.rs:204, 580). */
+int hbrbc_merkle_batch(hbrbc_ctx *ctx, const uint8_t *shards, size_t shard_len,
+                       size_t shard_stride, size_t inst_stride, size_t count, uint8_t *nodes,
+                       size_t node_inst_stride, void *stream);
+/* MerkleTree::proof for every index of every instance (broadcast.rs:212-222).
+ * proof (i, j): digests at digests + ((i*n + j)*max_proof_len(n))*32,
+ * count in ndig[i*n + j]. */
+int hbrbc_proofs_batch(hbrbc_ctx *ctx, const uint8_t *nodes, size_t node_inst_stride,
+                       size_t count, uint8_t *digests, uint8_t *ndig, void *stream);
+/* Proof::validate for `count` x `per_inst` proofs (broadcast.rs:254, 291,
+ * 604-606).  Proof (i, j): value at values + i*value_inst_stride +
+ * j*value_stride (value_len bytes, value_stride % 8 == 0), index
+ * indices[i*per_inst + j] (NULL: index = j), digests/ndig laid out as
+ * hbrbc_proofs_batch with digest slots = max_proof_len(tree_n), root at
+ * roots + i*root_stride.  ok_out[i*per_inst + j] = 1 valid / 0 invalid. */
+int hbrbc_validate_batch(hbrbc_ctx *ctx, const uint8_t *values, size_t value_len,
+                         size_t value_stride, size_t value_inst_stride, size_t per_inst,
+                         const uint32_t *indices, const uint8_t *digests, const uint8_t *ndig,
+                         const uint8_t *roots, size_t root_stride, size_t tree_n, size_t count,
+                         uint8_t *ok_out, void *stream);
+/* Coding::reconstruct_shards over `count` instances (broadcast.rs:569):
+ * present[i*n + j] != 0 marks shard j of instance i as received; missing
+ * rows are overwritten in place (data from the first `data` present rows via
+ * inv(M[valid]), parity from the rebuilt data: bit-identical to rse).
+ * status_out[i] = HBRBC_OK or HBRBC_E_TOO_FEW_SHARDS_PRESENT.  Uses the
+ * context's workspace (grown on demand, the only allocation on this path;
+ * call hbrbc_reserve first to keep it out of a captured region). */
+int hbrbc_reconstruct_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len,
+                            size_t shard_stride, size_t inst_stride, const uint8_t *present,
+                            size_t count, int32_t *status_out, void *stream);
+/* decode_from_shards (broadcast.rs:563-601): reconstruct, re-tree over all n
+ * shards, compare with roots[i*root_stride..+32], unframe.  payload bytes of
+ * instance i go to payload_out + i*payload_stride (payload_stride >=
+ * data*shard_len rounded up to 4), their length to payload_len_out[i] and
+ * the outcome to status_out[i] (OK, TOO_FEW_SHARDS_PRESENT, ROOT_MISMATCH,
+ * NO_PAYLOAD_LEN).  `nodes` (count x node_inst_stride) receives the
+ * re-built trees. */
+int hbrbc_decode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                       size_t inst_stride, const uint8_t *present, size_t count,
+                       const uint8_t *roots, size_t root_stride, uint8_t *nodes,
+                       size_t node_inst_stride, uint8_t *payload_out, size_t payload_stride,
+                       uint32_t *payload_len_out, int32_t *status_out, void *stream);
+/* Pre-size the reconstruct workspace for `count` instances. */
+int hbrbc_reserve(hbrbc_ctx *ctx, size_t count);
+
+/* ---- measurement hooks (bench.py) --------------------------------------- */
+/* Stage ids for the per-stage device timers. */
+enum hbrbc_stage {
+    HBRBC_STAGE_FRAME = 0,
+    HBRBC_STAGE_ENCODE = 1,
+    HBRBC_STAGE_LEAF_HASH = 2,
+    HBRBC_STAGE_TREE_LEVELS = 3,
+    HBRBC_STAGE_PROOFS = 4,
+    HBRBC_STAGE_VALIDATE = 5,
+    HBRBC_STAGE_DECODE_MATRIX = 6,
+    HBRBC_STAGE_RECONSTRUCT = 7,
+    HBRBC_STAGE_UNFRAME = 8,
+    HBRBC_STAGE_COUNT = 9
+};
+/* When enabled, every stage's kernels are bracketed by hipEvents recorded on
+ * the stream they run on.  hbrbc_profile_read synchronises those events and
+ * returns total milliseconds and launch count per stage since the last
+ * reset. */
+int hbrbc_profile_enable(hbrbc_ctx *ctx, int enable);
+int hbrbc_profile_reset(hbrbc_ctx *ctx);
+int hbrbc_profile_read(hbrbc_ctx *ctx, double *ms_out, uint64_t *launches_out);
+const char *hbrbc_stage_name(int stage);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBRBC_H */

@@ -1,0 +1,84 @@
+"""CPU-side checks of the C ABI (no GPU compute): the library builds, loads and
+exports every symbol include/hbrbc.h declares; pure host helpers agree with
+the oracle; compute entry points fail loudly (no CPU fallback) without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import __graft_entry__
+import hbbft_amd as hb
+from oracle import pyoracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    __graft_entry__.build()
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "hbrbc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hbrbc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    L = ctypes.CDLL(hb.LIB_PATH)
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_library_is_gfx950_code_object():
+    data = open(hb.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_host_helpers_match_oracle():
+    L = hb.lib()
+    assert L.hbrbc_version().startswith(b"hbrbc")
+    for n in [1, 2, 3, 4, 5, 7, 8, 9, 17, 64, 128, 250, 256, 1000]:
+        assert L.hbrbc_merkle_node_count(n) == orc.merkle_node_count(n) == hb.merkle_node_count(n)
+        assert L.hbrbc_merkle_max_proof_len(n) == hb.max_proof_len(n)
+    for plen, k in [(0, 1), (1024, 2), (1 << 20, 6), (256 << 10, 22), (4 << 20, 84)]:
+        assert L.hbrbc_shard_len(plen, k) == orc.shard_len(plen, k) == hb.shard_len(plen, k)
+    assert [L.hbrbc_stage_name(i).decode() for i in range(9)] == hb.STAGES
+
+
+def test_merkle_proof_is_host_data_movement():
+    """MerkleTree::proof only copies sibling digests: checkable without a GPU."""
+    for n in [1, 4, 7, 9, 17, 64, 250]:
+        values = [bytes([i % 256, i // 256]) for i in range(n)]
+        nodes = orc.merkle_build(values)
+        for i in range(n):
+            dig = np.zeros((64, 32), np.uint8)
+            nd = ctypes.c_size_t(0)
+            st = hb.lib().hbrbc_merkle_proof(nodes.ctypes.data, n, i, dig.ctypes.data,
+                                             ctypes.byref(nd))
+            assert st == 0
+            assert np.array_equal(dig[: nd.value], orc.merkle_proof(nodes, n, i))
+        nd = ctypes.c_size_t(0)
+        assert hb.lib().hbrbc_merkle_proof(nodes.ctypes.data, n, n, None, ctypes.byref(nd)) == 13
+
+
+def test_rse_constructor_errors_precede_device():
+    """ReedSolomon::new argument errors are reported before any device use."""
+    h = ctypes.c_void_p()
+    assert hb.lib().hbrbc_coding_new(0, 3, -1, ctypes.byref(h)) == 3      # TooFewDataShards
+    assert hb.lib().hbrbc_coding_new(200, 57, -1, ctypes.byref(h)) == 2   # TooManyShards
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(hb.RseError) as e:
+        hb.Coding(4, 2)
+    assert e.value.code == 102  # NoDevice: fails loudly, never computes on the host
+    with pytest.raises(hb.HbrbcUnavailable):
+        hb.RbcBatch(16)

@@ -1,0 +1,302 @@
+"""GPU parity: the HIP path (libhbrbc.so via the C ABI) against the CPU oracle
+and the golden fixtures.  Integer/byte work: every comparison is bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import hbbft_amd as hb
+from oracle import pyoracle as orc
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    with open(os.path.join(G, name)) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    return torch
+
+
+# ---------------------------------------------------------------- Coding ---
+def test_encoding_matrix_matches_oracle(torch_cuda):
+    for k, m in [(1, 1), (2, 2), (5, 5), (6, 10), (22, 42), (44, 84), (84, 166), (86, 170),
+                 (200, 56), (255, 1)]:
+        assert np.array_equal(hb.Coding(k, m).encoding_matrix(), orc.build_matrix(k, k + m)), (k, m)
+
+
+def test_encode_kat_5_5(torch_cuda):
+    kat = load("rs_kat.json")["encode_5_5"]
+    shards = [np.array(r, np.uint8) for r in kat["data"]] + [np.zeros(2, np.uint8) for _ in range(5)]
+    hb.Coding(5, 5).encode(shards)
+    assert [s.tolist() for s in shards[5:]] == kat["parity"]
+
+
+@pytest.mark.parametrize("k,m,L", [(2, 2, 1), (2, 2, 514), (6, 10, 1000), (22, 42, 11916),
+                                   (44, 84, 333), (84, 166, 97), (3, 1, 17), (128, 128, 64),
+                                   (1, 255, 33)])
+def test_coding_encode_reconstruct_vs_oracle(torch_cuda, k, m, L):
+    rng = np.random.default_rng(k * 1000 + m + L)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    gpu = [d.copy() for d in data] + [np.full(L, 0xEE, np.uint8) for _ in range(m)]
+    hb.Coding(k, m).encode(gpu)
+    st, ref = orc.rs_encode(k, m, [d.copy() for d in data] + [np.zeros(L, np.uint8)
+                                                             for _ in range(m)])
+    assert st == 0
+    for a, b in zip(gpu, ref):
+        assert np.array_equal(a, b)
+    # reconstruct from several erasure patterns, incl. worst case (only parity)
+    coding = hb.Coding(k, m)
+    n = k + m
+    pats = [rng.permutation(n)[: rng.integers(1, m + 1)] for _ in range(3)]
+    if m >= k:
+        pats.append(np.arange(k))  # every data shard missing
+    for erase in pats:
+        opt = [None if i in set(erase.tolist()) else ref[i].tobytes() for i in range(n)]
+        coding.reconstruct_shards(opt)
+        assert all(opt[i] == ref[i].tobytes() for i in range(n)), (k, m, erase)
+
+
+def test_reconstruct_errors_match_rse(torch_cuda):
+    c = hb.Coding(4, 2)
+    sh = [bytes([i] * 8) for i in range(6)]
+    with pytest.raises(hb.RseError) as e:
+        c.reconstruct_shards([sh[0], None, None, None, sh[4], sh[5]])
+    assert e.value.code == 10  # TooFewShardsPresent
+    with pytest.raises(hb.RseError) as e:
+        c.reconstruct_shards([sh[0], sh[1][:4], None, sh[3], sh[4], sh[5]])
+    assert e.value.code == 9   # IncorrectShardSize
+    with pytest.raises(hb.RseError) as e:
+        c.reconstruct_shards([b"", None, sh[2], sh[3], sh[4], sh[5]])
+    assert e.value.code == 11  # EmptyShard
+    with pytest.raises(hb.RseError) as e:
+        c.reconstruct_shards(sh[:5])
+    assert e.value.code == 1   # TooFewShards
+    with pytest.raises(hb.RseError) as e:
+        c.encode([bytearray(8) for _ in range(7)])
+    assert e.value.code == 2   # TooManyShards
+    with pytest.raises(hb.RseError) as e:
+        c.encode([bytearray(8)] * 5 + [bytearray(7)])
+    assert e.value.code == 9
+    # Coding::Trivial (broadcast.rs:677, 685-690)
+    t = hb.Coding(3, 0)
+    t.encode([bytearray(b"a"), bytearray(b"bc"), bytearray(b"")])
+    t.reconstruct_shards([b"a", b"b", b"c"])
+    with pytest.raises(hb.RseError) as e:
+        t.reconstruct_shards([b"a", None, b"c"])
+    assert e.value.code == 10
+
+
+# ---------------------------------------------------------------- Merkle ---
+def test_merkle_shapes_golden(torch_cuda):
+    """merkle.rs:152-166 test_merkle on the GPU, digests pinned by hashlib."""
+    shapes = load("merkle_shapes.json")
+    for n_s, case in shapes.items():
+        n = int(n_s)
+        tree = hb.MerkleTree.from_vec([bytes([i]) for i in range(n)])
+        assert tree.root_hash().hex() == case["root"]
+        for i in range(n):
+            p = tree.proof(i)
+            assert [d.hex() for d in p.digests()] == case["proofs"][i]
+            assert p.validate(n)
+        assert tree.proof(n) is None
+
+
+def test_merkle_ragged_values_vs_oracle(torch_cuda):
+    rng = np.random.default_rng(5)
+    for n in [1, 2, 3, 6, 33, 100]:
+        vals = [rng.integers(0, 256, int(rng.integers(0, 700)), dtype=np.uint8).tobytes()
+                for _ in range(n)]
+        tree = hb.MerkleTree.from_vec(vals)
+        ref = orc.merkle_build(vals)
+        assert tree.root_hash() == ref[-1].tobytes()
+        lv = tree.levels()
+        assert [d for level in lv for d in level] == [r.tobytes() for r in ref]
+
+
+def test_sha3_rate_boundaries_golden(torch_cuda):
+    kat = load("sha3_kat.json")
+    vals = [bytes((7 * i + 3) & 0xFF for i in range(L)) for L in range(301)]
+    tree = hb.MerkleTree.from_vec(vals)
+    assert [d.hex() for d in tree.levels()[0]] == kat["digests"]
+
+
+def test_proof_validate_rejections(torch_cuda):
+    n = 9
+    tree = hb.MerkleTree.from_vec([bytes([i]) for i in range(n)])
+    p = tree.proof(3)
+    root = tree.root_hash()
+    assert p.validate(n)
+    assert not hb.Proof(bytes([4]), 3, p.digests(), root).validate(n)
+    assert not hb.Proof(bytes([3]), 2, p.digests(), root).validate(n)
+    assert not hb.Proof(bytes([3]), 3, p.digests()[:-1], root).validate(n)
+    assert not hb.Proof(bytes([3]), 3, p.digests() + p.digests()[:1], root).validate(n)
+    assert not hb.Proof(bytes([3]), 3, p.digests() * 40, root).validate(n)
+    assert not hb.Proof(bytes([3]), 3, p.digests(), root).validate(2 * n)
+    bad = bytearray(p.digests()[0])
+    bad[0] ^= 1
+    assert not hb.Proof(bytes([3]), 3, [bytes(bad)] + p.digests()[1:], root).validate(n)
+    # index n-1 of an odd tree has a short proof (promoted node)
+    assert len(tree.proof(8).digests()) == 1 and tree.proof(8).validate(n)
+
+
+# ----------------------------------------------------------- batched path ---
+def run_pipeline(torch, n, f, plen, count, seed, erase_seed, n_erase, garbage=0xA5):
+    rb = hb.RbcBatch(n, f, device=0)
+    k = rb.k
+    S = hb.shard_len(plen, k)
+    pay = np.stack([orc.gen_payload(seed, i, plen) for i in range(count)]) if plen else \
+        np.zeros((count, 0), np.uint8)
+    pstride = max(16, (plen + 15) // 16 * 16)
+    payloads = torch.zeros((count, pstride), dtype=torch.uint8, device="cuda")
+    if plen:
+        payloads[:, :plen] = torch.from_numpy(pay).cuda()
+    slab = rb.alloc_slab(count, S)
+    slab.fill_(0x5A)  # poison: framing must zero every padding byte
+    nodes = rb.alloc_nodes(count)
+    rb.frame(payloads, plen, slab)
+    rb.encode(slab, S)
+    rb.merkle(slab, S, nodes)
+    ds = max(rb.dslots, 1)
+    digests = torch.zeros((count, n, ds, 32), dtype=torch.uint8, device="cuda")
+    ndig = torch.zeros((count, n), dtype=torch.uint8, device="cuda")
+    rb.proofs(nodes, digests, ndig)
+    ok = torch.zeros((count, n), dtype=torch.uint8, device="cuda")
+    rb.validate(slab, S, digests, ndig, nodes, ok)
+    present = np.stack([orc.gen_present(erase_seed, i, n, n_erase) for i in range(count)])
+    pres_d = torch.from_numpy(present).cuda()
+    roots = nodes[:, -1, :].clone()
+    recv = slab.clone()
+    recv[pres_d == 0] = garbage
+    nodes2 = rb.alloc_nodes(count)
+    ostride = max(16, (k * S + 15) // 16 * 16)
+    out = torch.zeros((count, ostride), dtype=torch.uint8, device="cuda")
+    plen_out = torch.zeros(count, dtype=torch.int32, device="cuda")
+    status = torch.zeros(count, dtype=torch.int32, device="cuda")
+    rb.decode(recv, S, pres_d, roots, nodes2, out, plen_out, status)
+    torch.cuda.synchronize()
+    return dict(rb=rb, S=S, pay=pay, slab=slab.cpu().numpy(), nodes=nodes.cpu().numpy(),
+                digests=digests.cpu().numpy(), ndig=ndig.cpu().numpy(), ok=ok.cpu().numpy(),
+                present=present, recv=recv.cpu().numpy(), nodes2=nodes2.cpu().numpy(),
+                out=out.cpu().numpy(), plen=plen_out.cpu().numpy(), status=status.cpu().numpy())
+
+
+@pytest.mark.parametrize("n,plen,count", [(1, 3, 3), (2, 0, 2), (3, 77, 3), (4, 1024, 5),
+                                          (4, 0, 2), (5, 300, 4), (7, 1001, 4), (8, 4099, 3),
+                                          (10, 500, 3), (16, 6001, 4), (31, 777, 3),
+                                          (64, 11916 * 22 - 4, 3), (64, 5000, 4),
+                                          (100, 2048, 3), (128, 10000, 3), (250, 20000, 2),
+                                          (256, 1234, 2)])
+def test_pipeline_vs_oracle(torch_cuda, n, plen, count):
+    f = (n - 1) // 3
+    r = run_pipeline(torch_cuda, n, f, plen, count, seed=0x48424246, erase_seed=11, n_erase=f)
+    S = r["S"]
+    dslots = hb.max_proof_len(n)
+    for i in range(count):
+        sh, nd = orc.send_shards(n, f, r["pay"][i].tobytes())
+        assert np.array_equal(r["slab"][i, :, :S], sh), (n, plen, i)
+        assert not r["slab"][i, :, S:].any(), "padding must be zero"
+        assert np.array_equal(r["nodes"][i], nd)
+        for j in range(n):
+            p = orc.merkle_proof(nd, n, j)
+            assert r["ndig"][i, j] == len(p)
+            if dslots:
+                assert np.array_equal(r["digests"][i, j, : len(p)], p)
+        assert r["ok"][i].all()
+        assert r["status"][i] == 0
+        assert r["plen"][i] == plen
+        assert np.array_equal(r["out"][i, :plen], r["pay"][i])
+        assert np.array_equal(r["recv"][i, :, :S], sh)
+        assert np.array_equal(r["nodes2"][i], nd)
+
+
+def test_pipeline_golden_vectors(torch_cuda):
+    """Roots / shard digests of the independent Python restatement (hashlib)."""
+    import hashlib
+    v = load("broadcast_vectors.json")
+    for c in v["cases"]:
+        n, f, plen, i = c["n"], c["f"], c["plen"], c["inst"]
+        r = run_pipeline(torch_cuda, n, f, plen, i + 1, seed=v["seed"], erase_seed=0, n_erase=0)
+        S = r["S"]
+        assert S == c["S"]
+        assert r["nodes"][i, -1].tobytes().hex() == c["root"], (n, plen)
+        assert [hashlib.sha3_256(r["slab"][i, j, :S].tobytes()).hexdigest()
+                for j in range(n)] == c["shard_sha3"]
+        for j_s, dig in c["proofs"].items():
+            j = int(j_s)
+            nd = r["ndig"][i, j]
+            assert [r["digests"][i, j, t].tobytes().hex() for t in range(nd)] == dig
+
+
+def test_worst_case_erasures_and_faults(torch_cuda):
+    torch = torch_cuda
+    n, f, plen, count = 16, 5, 3000, 6
+    r = run_pipeline(torch, n, f, plen, count, seed=3, erase_seed=4, n_erase=2 * f)
+    assert (r["status"] == 0).all() and (r["plen"] == plen).all()
+    for i in range(count):
+        assert np.array_equal(r["out"][i, :plen], r["pay"][i])
+    # too few shards present -> TooFewShardsPresent; tampered shard -> root mismatch
+    rb = r["rb"]
+    S = r["S"]
+    slab = torch.from_numpy(r["slab"]).cuda()
+    roots = torch.from_numpy(r["nodes"][:, -1, :].copy()).cuda()
+    present = torch.ones((count, n), dtype=torch.uint8, device="cuda")
+    present[0, : 2 * f + 1] = 0            # only k-1 present
+    slab[1, n - 1, 0] ^= 1                  # corrupt a parity shard that is used
+    present[1, :f] = 0
+    slab[2, 0, 0] ^= 0xFF                   # corrupt the length prefix (root mismatch)
+    nodes2 = rb.alloc_nodes(count)
+    out = torch.zeros((count, (rb.k * S + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+    plen_out = torch.zeros(count, dtype=torch.int32, device="cuda")
+    status = torch.zeros(count, dtype=torch.int32, device="cuda")
+    rb.decode(slab, S, present, roots, nodes2, out, plen_out, status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert st[0] == 10 and st[1] == 65 and st[2] == 65
+    assert (st[3:] == 0).all()
+
+
+def test_batched_validate_rejects_bad_proofs(torch_cuda):
+    torch = torch_cuda
+    n, f, plen, count = 64, 21, 20000, 2
+    r = run_pipeline(torch, n, f, plen, count, seed=5, erase_seed=6, n_erase=f)
+    rb, S = r["rb"], r["S"]
+    slab = torch.from_numpy(r["slab"]).cuda()
+    nodes = torch.from_numpy(r["nodes"]).cuda()
+    digests = torch.from_numpy(r["digests"]).cuda()
+    ndig = torch.from_numpy(r["ndig"]).cuda()
+    slab[0, 5, 17] ^= 0x10                     # wrong value
+    digests[0, 9, 2, 0] ^= 1                   # wrong sibling
+    ndig[1, 3] -= 1                            # too few digests
+    idx = torch.arange(n, dtype=torch.int32, device="cuda").repeat(count, 1)
+    idx[1, 7] = 8                              # wrong index
+    ok = torch.zeros((count, n), dtype=torch.uint8, device="cuda")
+    rb.validate(slab, S, digests, ndig, nodes, ok, indices=idx)
+    torch.cuda.synchronize()
+    okh = ok.cpu().numpy()
+    bad = {(0, 5), (0, 9), (1, 3), (1, 7)}
+    for i in range(count):
+        for j in range(n):
+            assert okh[i, j] == (0 if (i, j) in bad else 1), (i, j)
+
+
+def test_full_size_roundtrip_properties(torch_cuda):
+    """BASELINE cfg3 sizes (N=64, 256 KiB): oracle-checked on a few instances,
+    size-independent properties (round trip, all proofs valid) on all."""
+    torch = torch_cuda
+    n, f, plen, count = 64, 21, 256 * 1024, 32
+    r = run_pipeline(torch, n, f, plen, count, seed=0x48424246, erase_seed=1, n_erase=f)
+    assert r["ok"].all()
+    assert (r["status"] == 0).all() and (r["plen"] == plen).all()
+    assert np.array_equal(r["out"][:, :plen], r["pay"])
+    for i in (0, count - 1):
+        sh, nd = orc.send_shards(n, f, r["pay"][i].tobytes())
+        assert np.array_equal(r["slab"][i, :, : r["S"]], sh)
+        assert np.array_equal(r["nodes"][i], nd)
