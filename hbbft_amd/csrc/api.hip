@@ -208,9 +208,9 @@ struct StageTimer {
     }
 };
 
-inline hipStream_t pick(hbrbc_ctx *c, void *stream) {
-    return stream ? static_cast<hipStream_t>(stream) : c->stream;
-}
+// NULL selects the HIP null (default) stream, as for hipMemcpyAsync; the
+// context's own stream is used only by the synchronous per-call shims.
+inline hipStream_t pick(hbrbc_ctx *, void *stream) { return static_cast<hipStream_t>(stream); }
 
 int check_slab(const void *base, size_t shard_len, size_t shard_stride, size_t inst_stride,
                size_t n, size_t count) {

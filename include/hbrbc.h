@@ -15,7 +15,7 @@
  *     the device and run the same HIP kernels as the batched layer.
  *  2. Batched entry points on DEVICE memory for thousands of independent
  *     broadcast instances per call (the hot path).  All are asynchronous on
- *     the given stream (a hipStream_t; NULL = the context's own stream) and
+ *     the given stream (a hipStream_t; NULL = the HIP null stream) and
  *     never allocate, free or synchronise unless documented.
  *
  * Batched layout ("shard slab"): instance `i`, shard `j`, byte `b` lives at
