@@ -154,6 +154,7 @@ struct DevBuf {
 struct hbrbc_ctx {
     int device = 0;
     size_t k = 0, m = 0, n = 0;
+    int rt_enc = 2, rt_rec = 2;  // GF row tiles (rows per pass) for encode / reconstruct
     std::vector<uint8_t> matrix;  // n x k
     hipStream_t stream = nullptr;
     DevBuf d_matrix, d_enc_tables, d_enc_in, d_enc_out;
@@ -238,10 +239,14 @@ int check_nodes(const void *nodes, size_t node_inst_stride, size_t n, size_t cou
     return HBRBC_OK;
 }
 
+size_t rec_tab_rows(const hbrbc_ctx *c) {
+    return (c->m + c->rt_rec - 1) / c->rt_rec * c->rt_rec;
+}
+
 int ensure_workspace(hbrbc_ctx *c, size_t count) {
     if (count <= c->ws_count) return HBRBC_OK;
     const size_t k = c->k, m = c->m;
-    HB_HIP(c->ws_tables.ensure(count * m * k * sizeof(uint4) + 16));
+    HB_HIP(c->ws_tables.ensure(count * rec_tab_rows(c) * k * sizeof(uint4) + 16));
     HB_HIP(c->ws_in.ensure(count * k + 16));
     HB_HIP(c->ws_out.ensure(count * m + 16));
     HB_HIP(c->ws_nout.ensure(count * sizeof(int)));
@@ -281,6 +286,7 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shar
         DecodeMatrixArgs a;
         a.n = (int)c->n;
         a.k = (int)c->k;
+        a.rt = c->rt_rec;
         a.matrix = c->d_matrix.as<uint8_t>();
         a.present = present;
         a.count = count;
@@ -299,7 +305,8 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shar
     g.shard_stride = shard_stride;
     g.n16 = (int)((shard_len + 15) / 16);
     g.tables = c->ws_tables.as<uint4>();
-    g.tab_inst_stride = c->m * c->k;
+    g.tab_inst_stride = rec_tab_rows(c) * c->k;
+    g.rt = c->rt_rec;
     g.in_idx = c->ws_in.as<uint8_t>();
     g.in_idx_stride = c->k;
     g.out_idx = c->ws_out.as<uint8_t>();
@@ -354,6 +361,11 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
     c->k = data_shards;
     c->m = parity_shards;
     c->n = data_shards + parity_shards;
+    c->rt_enc = gf_row_tile((int)c->m);
+    // reconstruct rebuilds f..2f rows per instance in hbbft (f random
+    // erasures typical); tile for the typical count, the worst case costs
+    // one more pass
+    c->rt_rec = gf_row_tile((int)((c->m + 1) / 2));
     if (!build_matrix(c->k, c->n, c->matrix)) {
         delete c;
         return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
@@ -369,10 +381,13 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
         guard(hipMemcpy(c->d_matrix.p, c->matrix.data(), c->matrix.size(), hipMemcpyHostToDevice));
     if (c->m > 0 && st == HBRBC_OK) {
         const HostGf &g = gf();
-        std::vector<uint4> tab(c->m * c->k);
+        // pass-major [pass][j][rt_enc] split-2-bit entries, zero-padded rows
+        const size_t rt = (size_t)c->rt_enc, npass = (c->m + rt - 1) / rt;
+        std::vector<uint4> tab(npass * rt * c->k, make_uint4(0, 0, 0, 0));
         for (size_t r = 0; r < c->m; ++r)
             for (size_t j = 0; j < c->k; ++j)
-                tab[r * c->k + j] = gf_split2_entry(c->matrix[(c->k + r) * c->k + j], g.exp, g.log);
+                tab[((r / rt) * c->k + j) * rt + (r % rt)] =
+                    gf_split2_entry(c->matrix[(c->k + r) * c->k + j], g.exp, g.log);
         std::vector<uint8_t> in(c->k), outi(c->m);
         for (size_t j = 0; j < c->k; ++j) in[j] = (uint8_t)j;
         for (size_t r = 0; r < c->m; ++r) outi[r] = (uint8_t)(c->k + r);
@@ -482,6 +497,7 @@ int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     g.n16 = (int)((shard_len + 15) / 16);
     g.tables = c->d_enc_tables.as<uint4>();
     g.tab_inst_stride = 0;
+    g.rt = c->rt_enc;
     g.in_idx = c->d_enc_in.as<uint8_t>();
     g.in_idx_stride = 0;
     g.out_idx = c->d_enc_out.as<uint8_t>();

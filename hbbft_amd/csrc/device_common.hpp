@@ -74,22 +74,28 @@ __device__ __forceinline__ void rotl64(uint32_t lo, uint32_t hi, uint32_t &ol, u
     HB_RHOPI(19, 13, 8);                                                                         \
     HB_RHOPI(24, 4, 14)
 
-// One Keccak-f[1600] permutation on a lane-private state.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // a ^ b ^ c in one VALU op
+}
+
+// One Keccak-f[1600] permutation on a lane-private state: 180 VALU ops per
+// round (theta 20 xor3 + 10 alignbit + 50 xor3, rho 48 alignbit, chi 50
+// bitop3, iota 2 xor).
 __device__ __forceinline__ void keccak_f1600(uint32_t (&L)[25], uint32_t (&H)[25]) {
 #pragma unroll 1
     for (int round = 0; round < 24; ++round) {
         uint32_t CL[5], CH[5], RL[5], RH[5];
 #pragma unroll
         for (int x = 0; x < 5; ++x) {
-            CL[x] = L[x] ^ L[x + 5] ^ L[x + 10] ^ L[x + 15] ^ L[x + 20];
-            CH[x] = H[x] ^ H[x + 5] ^ H[x + 10] ^ H[x + 15] ^ H[x + 20];
+            CL[x] = xor3(xor3(L[x], L[x + 5], L[x + 10]), L[x + 15], L[x + 20]);
+            CH[x] = xor3(xor3(H[x], H[x + 5], H[x + 10]), H[x + 15], H[x + 20]);
         }
 #pragma unroll
         for (int x = 0; x < 5; ++x) rotl64<1>(CL[(x + 1) % 5], CH[(x + 1) % 5], RL[x], RH[x]);
 #pragma unroll
         for (int i = 0; i < 25; ++i) {
-            L[i] = L[i] ^ CL[(i + 4) % 5] ^ RL[i % 5];
-            H[i] = H[i] ^ CH[(i + 4) % 5] ^ RH[i % 5];
+            L[i] = xor3(L[i], CL[(i + 4) % 5], RL[i % 5]);
+            H[i] = xor3(H[i], CH[(i + 4) % 5], RH[i % 5]);
         }
         uint32_t BL[25], BH[25];
         HB_RHOPI_ALL;
@@ -117,13 +123,11 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     const uint2 *q = reinterpret_cast<const uint2 *>(p);
     const uint32_t nfull = len / 136u;
     for (uint32_t t = 0; t < nfull; ++t) {
-        uint2 v[17];
-#pragma unroll
-        for (int w = 0; w < 17; ++w) v[w] = q[w];
 #pragma unroll
         for (int w = 0; w < 17; ++w) {
-            L[w] ^= v[w].x;
-            H[w] ^= v[w].y;
+            const uint2 v = q[w];
+            L[w] ^= v.x;
+            H[w] ^= v.y;
         }
         q += 17;
         keccak_f1600(L, H);

@@ -78,9 +78,12 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(
 
 // -------------------------------------------------------------- GF apply --
 // Split-2-bit v_perm_b32 GF(2^8) multiply-accumulate over 16-byte chunks.
-// Every lane owns 16 consecutive byte positions of all rows; a table entry
-// (4 dwords, scalar-loaded) turns 4 packed bytes into c*x with 4 v_perm_b32
-// and 2 v_xor3_b32.  RT output rows are accumulated per pass.
+// Every lane owns 16 consecutive byte positions of all rows.  Output rows
+// are produced RT at a time ("passes"); the tables are pass-major
+// [pass][input j][RT] so the RT entries for one input arrive as wide scalar
+// loads.  Per (row, input, dword): 4 v_perm_b32 + 2 v_bitop3 (xor3) = 6 VALU
+// for 4 byte-MACs.  Rows past `nout` in the last pass carry zero entries;
+// only their stores are skipped.
 template <int RT>
 __global__ __launch_bounds__(kBlock) void gf_apply_kernel(
     uint8_t *__restrict__ base, size_t inst_stride, size_t shard_stride, int n16,
@@ -89,51 +92,54 @@ __global__ __launch_bounds__(kBlock) void gf_apply_kernel(
     const uint8_t *__restrict__ out_idx, size_t out_idx_stride,
     const int *__restrict__ nout_arr, int nout_uniform, int nin, int blocks_per_row) {
     const size_t inst = blockIdx.x / blocks_per_row;
-    const int chunk = (int)(blockIdx.x % blocks_per_row) * kBlock + (int)threadIdx.x;
-    const bool active = chunk < n16;
+    const int chunk0 = (int)(blockIdx.x % blocks_per_row) * kBlock + (int)threadIdx.x;
+    const bool active = chunk0 < n16;
+    const int chunk = active ? chunk0 : n16 - 1;  // clamped: loads stay in bounds
     uint8_t *ib = base + inst * inst_stride;
     const int nout = nout_arr ? nout_arr[inst] : nout_uniform;
+    const int npass = (nout + RT - 1) / RT;
     const uint4 *tab = tables + inst * tab_inst_stride;
     const uint8_t *iidx = in_idx + inst * in_idx_stride;
     const uint8_t *oidx = out_idx + inst * out_idx_stride;
     const size_t off = (size_t)chunk * 16;
-    for (int r0 = 0; r0 < nout; r0 += RT) {
+    for (int p = 0; p < npass; ++p) {
         uint32_t acc[RT][4];
 #pragma unroll
-        for (int r = 0; r < RT; ++r)
+        for (int t = 0; t < RT; ++t)
 #pragma unroll
-            for (int d = 0; d < 4; ++d) acc[r][d] = 0u;
+            for (int d = 0; d < 4; ++d) acc[t][d] = 0u;
+        const uint4 *tp = tab + (size_t)p * nin * RT;
+        uint4 xn = *reinterpret_cast<const uint4 *>(ib + (size_t)iidx[0] * shard_stride + off);
         for (int j = 0; j < nin; ++j) {
-            const int src = iidx[j];
-            uint4 x = make_uint4(0, 0, 0, 0);
-            if (active) x = *reinterpret_cast<const uint4 *>(ib + (size_t)src * shard_stride + off);
+            const uint4 x = xn;
+            if (j + 1 < nin)
+                xn = *reinterpret_cast<const uint4 *>(ib + (size_t)iidx[j + 1] * shard_stride + off);
             const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
             uint32_t sel[4][4];
 #pragma unroll
             for (int d = 0; d < 4; ++d)
 #pragma unroll
                 for (int f = 0; f < 4; ++f) sel[f][d] = (xs[d] >> (2 * f)) & 0x03030303u;
+            const uint4 *tj = tp + (size_t)j * RT;
 #pragma unroll
-            for (int r = 0; r < RT; ++r) {
-                if (r0 + r < nout) {
-                    const uint4 t = tab[(size_t)(r0 + r) * nin + j];
+            for (int t = 0; t < RT; ++t) {
+                const uint4 e = tj[t];
 #pragma unroll
-                    for (int d = 0; d < 4; ++d) {
-                        acc[r][d] ^= __builtin_amdgcn_perm(t.x, t.x, sel[0][d]) ^
-                                     __builtin_amdgcn_perm(t.y, t.y, sel[1][d]) ^
-                                     __builtin_amdgcn_perm(t.z, t.z, sel[2][d]) ^
-                                     __builtin_amdgcn_perm(t.w, t.w, sel[3][d]);
-                    }
+                for (int d = 0; d < 4; ++d) {
+                    acc[t][d] = xor3(acc[t][d], __builtin_amdgcn_perm(e.x, e.x, sel[0][d]),
+                                     __builtin_amdgcn_perm(e.y, e.y, sel[1][d]));
+                    acc[t][d] = xor3(acc[t][d], __builtin_amdgcn_perm(e.z, e.z, sel[2][d]),
+                                     __builtin_amdgcn_perm(e.w, e.w, sel[3][d]));
                 }
             }
         }
         if (active) {
 #pragma unroll
-            for (int r = 0; r < RT; ++r) {
-                if (r0 + r < nout) {
-                    const int dst = oidx[r0 + r];
+            for (int t = 0; t < RT; ++t) {
+                if (p * RT + t < nout) {
+                    const int dst = oidx[p * RT + t];
                     *reinterpret_cast<uint4 *>(ib + (size_t)dst * shard_stride + off) =
-                        make_uint4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+                        make_uint4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
                 }
             }
         }
@@ -265,9 +271,10 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(
 // rows equal rse's parity-from-rebuilt-data by linearity over GF(2^8)),
 // expanded to split-2-bit tables for gf_apply_kernel.
 __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
-    int n, int k, const uint8_t *__restrict__ matrix, const uint8_t *__restrict__ present,
-    uint4 *__restrict__ tables, uint8_t *__restrict__ in_idx, uint8_t *__restrict__ out_idx,
-    int *__restrict__ nout, int32_t *__restrict__ status) {
+    int n, int k, int rt, const uint8_t *__restrict__ matrix,
+    const uint8_t *__restrict__ present, uint4 *__restrict__ tables,
+    uint8_t *__restrict__ in_idx, uint8_t *__restrict__ out_idx, int *__restrict__ nout,
+    int32_t *__restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *exp_t = smem;             // 512
     uint8_t *log_t = smem + 512;       // 256
@@ -356,19 +363,23 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
         }
         __syncthreads();
     }
-    uint4 *tab = tables + inst * (size_t)m * k;
-    for (int e = tid; e < nm * k; e += kBlock) {
+    const int npass = (m + rt - 1) / rt;
+    uint4 *tab = tables + inst * (size_t)npass * rt * k;
+    const int nrows = (nm + rt - 1) / rt * rt;  // pad the last pass with zero rows
+    for (int e = tid; e < nrows * k; e += kBlock) {
         const int t = e / k, c = e - t * k;
-        const int row = missing[t];
+        const int row = t < nm ? missing[t] : -1;
         uint8_t coef;
-        if (row < k) {
+        if (row < 0) {
+            coef = 0;
+        } else if (row < k) {
             coef = aug[row * w2 + k + c];
         } else {
             coef = 0;
             const uint8_t *mr = matrix + (size_t)row * k;
             for (int j = 0; j < k; ++j) coef ^= gf_mul_lds(exp_t, log_t, mr[j], aug[j * w2 + k + c]);
         }
-        tab[e] = gf_split2_entry(coef, exp_t, log_t);
+        tab[((size_t)(t / rt) * k + c) * rt + (t % rt)] = gf_split2_entry(coef, exp_t, log_t);
     }
     for (int j = tid; j < k; j += kBlock) in_idx[inst * (size_t)k + j] = valid[j];
     for (int t = tid; t < nm; t += kBlock) out_idx[inst * (size_t)m + t] = missing[t];
@@ -478,23 +489,38 @@ hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t p
 
 hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     if (a.count == 0 || a.n16 == 0) return hipSuccess;
+    if (!a.nout && a.nout_uniform == 0) return hipSuccess;
     const int bpr = (a.n16 + kBlock - 1) / kBlock;
     const size_t blocks = (size_t)bpr * a.count;
-    const int maxout = a.nout ? 256 : a.nout_uniform;
-    if (maxout == 0) return hipSuccess;
-#define HB_GF_LAUNCH(RT)                                                                         \
-    hipLaunchKernelGGL(gf_apply_kernel<RT>, dim3((unsigned)blocks), dim3(kBlock), 0, s, a.base, \
-                       a.inst_stride, a.shard_stride, a.n16, a.tables, a.tab_inst_stride,        \
-                       a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,           \
-                       a.nout_uniform, a.nin, bpr)
-    if (maxout <= 4)
-        HB_GF_LAUNCH(4);
-    else if (maxout <= 8)
-        HB_GF_LAUNCH(8);
-    else
-        HB_GF_LAUNCH(16);
-#undef HB_GF_LAUNCH
+#define HB_GF_CASE(RT)                                                                           \
+    case RT:                                                                                     \
+        hipLaunchKernelGGL(gf_apply_kernel<RT>, dim3((unsigned)blocks), dim3(kBlock), 0, s,      \
+                           a.base, a.inst_stride, a.shard_stride, a.n16, a.tables,               \
+                           a.tab_inst_stride, a.in_idx, a.in_idx_stride, a.out_idx,              \
+                           a.out_idx_stride, a.nout, a.nout_uniform, a.nin, bpr);                \
+        break
+    switch (a.rt) {
+        HB_GF_CASE(2);
+        HB_GF_CASE(4);
+        HB_GF_CASE(6);
+        HB_GF_CASE(8);
+        HB_GF_CASE(10);
+        HB_GF_CASE(12);
+        HB_GF_CASE(14);
+        HB_GF_CASE(16);
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef HB_GF_CASE
     return hipGetLastError();
+}
+
+int gf_row_tile(int rows) {
+    if (rows <= 0) return 2;
+    const int passes = (rows + 15) / 16;
+    int rt = (rows + passes - 1) / passes;
+    rt = (rt + 1) & ~1;
+    return rt < 2 ? 2 : (rt > 16 ? 16 : rt);
 }
 
 hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, size_t shard_stride,
@@ -551,7 +577,7 @@ hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
     hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(kBlock), lds, s, a.n,
-                       a.k, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
+                       a.k, a.rt, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
     return hipGetLastError();
 }
 

@@ -19,7 +19,7 @@ struct GfApplyArgs {
     uint8_t *base;
     size_t inst_stride, shard_stride;
     int n16;                    // 16-byte chunks per row
-    const uint4 *tables;        // split-2-bit entries [inst][row][nin]
+    const uint4 *tables;        // split-2-bit entries [inst][pass][nin][rt]
     size_t tab_inst_stride;     // in entries (0: shared)
     const uint8_t *in_idx;      // [inst][nin]
     size_t in_idx_stride;       // 0: shared
@@ -28,8 +28,11 @@ struct GfApplyArgs {
     const int *nout;            // [inst] or nullptr
     int nout_uniform;
     int nin;
+    int rt;                     // rows per pass: one of 2,4,...,16
     size_t count;
 };
+// Row tile for `rows` output rows: fewest passes of <= 16, evened out.
+int gf_row_tile(int rows);
 hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s);
 
 // SHA3 of every shard row -> level 0 of each instance's node slab.
@@ -62,11 +65,11 @@ hipError_t launch_validate(const ValidateArgs &a, hipStream_t s);
 // Per-instance decode matrix: inv(M[first k present]) applied to
 // M[missing rows] -> split-2-bit tables + row index lists.
 struct DecodeMatrixArgs {
-    int n, k;
+    int n, k, rt;
     const uint8_t *matrix;      // n x k encoding matrix (device)
     const uint8_t *present;     // [count][n]
     size_t count;
-    uint4 *tables;              // [count][m][k]
+    uint4 *tables;              // [count][ceil(m/rt)][k][rt]
     uint8_t *in_idx;            // [count][k]
     uint8_t *out_idx;           // [count][m]
     int *nout;                  // [count]
