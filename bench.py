@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-batches per step, each on its own HIP stream (overlap)")
     return ap.parse_args()
 
 
@@ -67,8 +69,11 @@ def main():
     n, plen, count, erase = CONFIGS[args.config]
     if args.count:
         count = args.count
+    nsub = max(1, min(args.streams, count))
     f = (n - 1) // 3
-    rb = hb.RbcBatch(n, f, device=local)
+    # one Coding context per sub-batch: each owns its reconstruct workspace
+    subs_rb = [hb.RbcBatch(n, f, device=local) for _ in range(nsub)]
+    rb = subs_rb[0]
     k, m = rb.k, rb.m
     S = hb.shard_len(plen, k)
     stride = rb.stride_for(S)
@@ -98,17 +103,41 @@ def main():
     out = torch.empty((count, ostride), dtype=torch.uint8, device=dev)
     plen_out = torch.empty(count, dtype=torch.int32, device=dev)
     status = torch.empty(count, dtype=torch.int32, device=dev)
-    rb.reserve(count)
-    stream = torch.cuda.current_stream(dev)
+
+    # sub-batches: contiguous instance ranges, one stream each, so one
+    # sub-batch's VALU-bound hashing overlaps another's HBM-bound copies and
+    # the grid tails of every stage fill (the work per step is unchanged)
+    bounds = [(i * count) // nsub for i in range(nsub + 1)]
+    main = torch.cuda.current_stream(dev)
+    subs = []
+    for i in range(nsub):
+        lo, hi = bounds[i], bounds[i + 1]
+        sb = subs_rb[i]
+        sb.reserve(hi - lo)
+        subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
+
+    def run_sub(sb, sl):
+        sb.frame(payloads[sl], plen, slab[sl])
+        sb.encode(slab[sl], S)
+        sb.merkle(slab[sl], S, nodes[sl])
+        sb.proofs(nodes[sl], digests[sl], ndig[sl])
+        sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
+        roots[sl].copy_(nodes[sl, -1, :])      # what the Echo/Ready quorum agreed on
+        sb.decode(slab[sl], S, present[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
+                  status[sl])
 
     def step():
-        rb.frame(payloads, plen, slab)
-        rb.encode(slab, S)
-        rb.merkle(slab, S, nodes)
-        rb.proofs(nodes, digests, ndig)
-        rb.validate(slab, S, digests, ndig, nodes, ok)
-        roots.copy_(nodes[:, -1, :])           # what the Echo/Ready quorum agreed on
-        rb.decode(slab, S, present, roots, nodes2, out, plen_out, status)
+        if nsub == 1:
+            run_sub(subs[0][0], subs[0][2])
+            return
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for sb, st, sl in subs:
+            st.wait_event(ev)
+            with torch.cuda.stream(st):
+                run_sub(sb, sl)
+        for _, st, _ in subs:
+            main.wait_stream(st)
 
     for _ in range(args.warmup):
         step()
@@ -119,8 +148,9 @@ def main():
         assert bool((plen_out == plen).all())
         assert torch.equal(out[:, :plen], payloads[:, :plen]), "decoded payload differs"
 
-    rb.profile(True)
-    rb.profile_reset()
+    for sb in subs_rb:
+        sb.profile(True)
+        sb.profile_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -129,37 +159,44 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    rb.profile(False)
+    for sb in subs_rb:
+        sb.profile(False)
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    stages = rb.profile_read()
+    stages = {}
+    for sb in subs_rb:
+        for st_name, (ms, cnt) in sb.profile_read().items():
+            a0, c0 = stages.get(st_name, (0.0, 0))
+            stages[st_name] = (a0 + ms, c0 + cnt)
 
     total_payload = float(count) * plen * world * args.steps
     value = total_payload / elapsed / 1e9
+    per_launch = count / nsub          # instances processed by one launch
 
     # ---- roofline of the dominant kernel (per launch, live HIP events) ---
     L = (S + 1 + 135) // 136  # Keccak blocks per leaf (S bytes + pad)
-    alg_bytes = {
-        "frame": count * (plen + k * stride),
-        "encode": count * (k + m) * stride,
-        "leaf_hash": count * n * (S + 32),
-        "tree_levels": count * (rb.node_count - n) * 96,
-        "proofs": count * (n * rb.dslots * 32 * 2 + n),
-        "validate": count * n * (S + 32 * (rb.dslots + 1) + 1),
-        "decode_matrix": count * (n + m * k * 16),
-        "reconstruct": count * (k + n_erase) * stride,
-        "unframe": count * (k * S + plen),
-    }
+    # algorithmic bytes per launch (SURVEY 8d per-instance figures x instances per launch)
+    alg_bytes = {s_: per_launch * v_ for s_, v_ in {
+        "frame": plen + k * S,
+        "encode": (k + m) * S,
+        "leaf_hash": n * (S + 32),
+        "tree_levels": (rb.node_count - n) * 96,   # one record = all levels of one tree batch
+        "proofs": n * rb.dslots * 32 * 2 + n,
+        "validate": n * (S + 32 * (rb.dslots + 1) + 1),
+        "decode_matrix": n + m * k * 16,
+        "reconstruct": (k + n_erase) * S,
+        "unframe": k * S + plen,
+    }.items()}
     dom = max(stages, key=lambda s: stages[s][0])
     dom_ms, dom_launches = stages[dom]
     per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
     achieved = alg_bytes[dom] / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    perms = {"leaf_hash": count * n * L, "validate": count * (n * L + n * rb.dslots),
-             "tree_levels": count * (n - 1)}
+    perms = {"leaf_hash": per_launch * n * L, "validate": per_launch * (n * L + n * rb.dslots),
+             "tree_levels": per_launch * (n - 1)}
     valu = None
     if dom in perms:
         ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
@@ -177,9 +214,9 @@ def main():
     if os.path.exists(prof):
         try:
             pm = json.load(open(prof))
-            key = "%s:%s:%d" % (args.config, dom, count)
-            if key in pm:
-                roofline["traffic"] = pm[key]
+            key = "%s:%s" % (args.config, dom)
+            if key in pm:   # HBM bytes per instance from the PMC pass x instances per launch
+                roofline["traffic"] = pm[key] * per_launch
         except Exception:
             pass
 
@@ -211,7 +248,8 @@ def main():
                                                     "f random" if erase == "f" else "worst-case"),
                        "n": n, "f": f, "payload_bytes": plen, "shard_len": S,
                        "instances_per_gpu": count, "global_batch": count * world,
-                       "parallelism": "instance-sharded x%d" % world},
+                       "parallelism": "instance-sharded x%d" % world,
+                       "streams_per_gpu": nsub},
             "roofline": roofline, "cpu_baseline": cpu,
             "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
         }

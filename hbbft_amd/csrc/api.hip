@@ -9,6 +9,8 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -155,6 +157,7 @@ struct hbrbc_ctx {
     int device = 0;
     size_t k = 0, m = 0, n = 0;
     int rt_enc = 2, rt_rec = 2;  // GF row tiles (rows per pass) for encode / reconstruct
+    int bitslice = 1;            // GF kernel: 1 bit-sliced (default), 0 split-2-bit v_perm
     std::vector<uint8_t> matrix;  // n x k
     hipStream_t stream = nullptr;
     DevBuf d_matrix, d_enc_tables, d_enc_in, d_enc_out;
@@ -247,8 +250,8 @@ int ensure_workspace(hbrbc_ctx *c, size_t count) {
     if (count <= c->ws_count) return HBRBC_OK;
     const size_t k = c->k, m = c->m;
     HB_HIP(c->ws_tables.ensure(count * rec_tab_rows(c) * k * sizeof(uint4) + 16));
-    HB_HIP(c->ws_in.ensure(count * k + 16));
-    HB_HIP(c->ws_out.ensure(count * m + 16));
+    HB_HIP(c->ws_in.ensure((count * k + 4) * sizeof(uint32_t)));
+    HB_HIP(c->ws_out.ensure((count * m + 4) * sizeof(uint32_t)));
     HB_HIP(c->ws_nout.ensure(count * sizeof(int)));
     HB_HIP(c->ws_status.ensure(count * sizeof(int32_t)));
     HB_HIP(c->ws_plen.ensure(count * sizeof(uint32_t)));
@@ -287,12 +290,13 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shar
         a.n = (int)c->n;
         a.k = (int)c->k;
         a.rt = c->rt_rec;
+        a.raw = c->bitslice;
         a.matrix = c->d_matrix.as<uint8_t>();
         a.present = present;
         a.count = count;
         a.tables = c->ws_tables.as<uint4>();
-        a.in_idx = c->ws_in.as<uint8_t>();
-        a.out_idx = c->ws_out.as<uint8_t>();
+        a.in_idx = c->ws_in.as<uint32_t>();
+        a.out_idx = c->ws_out.as<uint32_t>();
         a.nout = c->ws_nout.as<int>();
         a.status = status;
         HB_HIP(launch_decode_matrix(a, s));
@@ -307,12 +311,14 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shar
     g.tables = c->ws_tables.as<uint4>();
     g.tab_inst_stride = rec_tab_rows(c) * c->k;
     g.rt = c->rt_rec;
-    g.in_idx = c->ws_in.as<uint8_t>();
+    g.bitslice = c->bitslice;
+    g.in_idx = c->ws_in.as<uint32_t>();
     g.in_idx_stride = c->k;
-    g.out_idx = c->ws_out.as<uint8_t>();
+    g.out_idx = c->ws_out.as<uint32_t>();
     g.out_idx_stride = c->m;
     g.nout = c->ws_nout.as<int>();
     g.nout_uniform = 0;
+    g.max_rows = (int)c->m;
     g.nin = (int)c->k;
     g.count = count;
     HB_HIP(launch_gf_apply(g, s));
@@ -366,6 +372,16 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
     // erasures typical); tile for the typical count, the worst case costs
     // one more pass
     c->rt_rec = gf_row_tile((int)((c->m + 1) / 2));
+    if (const char *e = getenv("HBRBC_GF")) {
+        // bitslice (uniform branches), bitslice_likely (set-bit path inline),
+        // bitslice_mask (branch-free masked xor), perm (split-2-bit v_perm)
+        if (!std::strcmp(e, "perm")) c->bitslice = 0;
+        else if (!std::strcmp(e, "bitslice_likely")) c->bitslice = 2;
+        else if (!std::strcmp(e, "bitslice_mask")) c->bitslice = 3;
+        else c->bitslice = 1;
+    }
+    if (const char *e = getenv("HBRBC_RT_ENC")) c->rt_enc = std::max(2, std::min(16, atoi(e) & ~1));
+    if (const char *e = getenv("HBRBC_RT_REC")) c->rt_rec = std::max(2, std::min(16, atoi(e) & ~1));
     if (!build_matrix(c->k, c->n, c->matrix)) {
         delete c;
         return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
@@ -381,24 +397,32 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
         guard(hipMemcpy(c->d_matrix.p, c->matrix.data(), c->matrix.size(), hipMemcpyHostToDevice));
     if (c->m > 0 && st == HBRBC_OK) {
         const HostGf &g = gf();
-        // pass-major [pass][j][rt_enc] split-2-bit entries, zero-padded rows
+        // pass-major tables, zero-padded rows: split-2-bit entries [pass][j][rt_enc]
+        // (v_perm kernel) or coefficient bytes [pass][j][16] (bit-sliced kernel)
         const size_t rt = (size_t)c->rt_enc, npass = (c->m + rt - 1) / rt;
         std::vector<uint4> tab(npass * rt * c->k, make_uint4(0, 0, 0, 0));
+        uint8_t *raw = reinterpret_cast<uint8_t *>(tab.data());
         for (size_t r = 0; r < c->m; ++r)
-            for (size_t j = 0; j < c->k; ++j)
-                tab[((r / rt) * c->k + j) * rt + (r % rt)] =
-                    gf_split2_entry(c->matrix[(c->k + r) * c->k + j], g.exp, g.log);
-        std::vector<uint8_t> in(c->k), outi(c->m);
-        for (size_t j = 0; j < c->k; ++j) in[j] = (uint8_t)j;
-        for (size_t r = 0; r < c->m; ++r) outi[r] = (uint8_t)(c->k + r);
+            for (size_t j = 0; j < c->k; ++j) {
+                const uint8_t coef = c->matrix[(c->k + r) * c->k + j];
+                if (c->bitslice)
+                    raw[((r / rt) * c->k + j) * 16 + (r % rt)] = coef;
+                else
+                    tab[((r / rt) * c->k + j) * rt + (r % rt)] = gf_split2_entry(coef, g.exp, g.log);
+            }
+        std::vector<uint32_t> in(c->k), outi(c->m);
+        for (size_t j = 0; j < c->k; ++j) in[j] = (uint32_t)j;
+        for (size_t r = 0; r < c->m; ++r) outi[r] = (uint32_t)(c->k + r);
         guard(c->d_enc_tables.ensure(tab.size() * sizeof(uint4)));
-        guard(c->d_enc_in.ensure(in.size()));
-        guard(c->d_enc_out.ensure(outi.size()));
+        guard(c->d_enc_in.ensure(in.size() * sizeof(uint32_t)));
+        guard(c->d_enc_out.ensure(outi.size() * sizeof(uint32_t)));
         if (st == HBRBC_OK) {
             guard(hipMemcpy(c->d_enc_tables.p, tab.data(), tab.size() * sizeof(uint4),
                             hipMemcpyHostToDevice));
-            guard(hipMemcpy(c->d_enc_in.p, in.data(), in.size(), hipMemcpyHostToDevice));
-            guard(hipMemcpy(c->d_enc_out.p, outi.data(), outi.size(), hipMemcpyHostToDevice));
+            guard(hipMemcpy(c->d_enc_in.p, in.data(), in.size() * sizeof(uint32_t),
+                            hipMemcpyHostToDevice));
+            guard(hipMemcpy(c->d_enc_out.p, outi.data(), outi.size() * sizeof(uint32_t),
+                            hipMemcpyHostToDevice));
         }
     }
     if (st != HBRBC_OK) {
@@ -498,12 +522,14 @@ int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     g.tables = c->d_enc_tables.as<uint4>();
     g.tab_inst_stride = 0;
     g.rt = c->rt_enc;
-    g.in_idx = c->d_enc_in.as<uint8_t>();
+    g.bitslice = c->bitslice;
+    g.in_idx = c->d_enc_in.as<uint32_t>();
     g.in_idx_stride = 0;
-    g.out_idx = c->d_enc_out.as<uint8_t>();
+    g.out_idx = c->d_enc_out.as<uint32_t>();
     g.out_idx_stride = 0;
     g.nout = nullptr;
     g.nout_uniform = (int)c->m;
+    g.max_rows = (int)c->m;
     g.nin = (int)c->k;
     g.count = count;
     HB_HIP(launch_gf_apply(g, s));
@@ -616,7 +642,7 @@ int hbrbc_decode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     st = check_nodes(nodes, node_inst_stride, c->n, count);
     if (st) return st;
     const size_t total = c->k * shard_len;
-    const size_t need = total >= 4 ? round_up(total - 4, 4) : 0;
+    const size_t need = total >= 4 ? round_up(total - 4, 16) : 0;  // 16-byte output chunks
     if (need && (!payload_out || reinterpret_cast<uintptr_t>(payload_out) % 4 ||
                  payload_stride % 4 || (count > 1 && payload_stride < need)))
         return fail(HBRBC_E_INVALID_ARG, "payload_out stride must be a multiple of 4 and >= %zu",

@@ -25,55 +25,61 @@ inline unsigned grid_for(size_t threads, size_t cap = 256 * 32) {
 }
 
 // ----------------------------------------------------------------- frame --
-// One thread per dword of every data row (grid-stride).  Logical framed
-// byte b (= BE32(len) ++ payload ++ 0s) lives in row b / S at b % S.
+// 16 contiguous bytes (one uint4 store) of 16 consecutive bytes from five aligned dword loads:
+// bytes [sh/8, sh/8 + 16) of the 20-byte little-endian window d[0..4].
+__device__ __forceinline__ uint4 funnel16(const uint32_t (&d)[5], uint32_t sh) {
+    if (sh == 0) return make_uint4(d[0], d[1], d[2], d[3]);
+    return make_uint4(__builtin_amdgcn_alignbit(d[1], d[0], sh),
+                      __builtin_amdgcn_alignbit(d[2], d[1], sh),
+                      __builtin_amdgcn_alignbit(d[3], d[2], sh),
+                      __builtin_amdgcn_alignbit(d[4], d[3], sh));
+}
+
+// One thread per 16-byte chunk of every data row; the (instance, row) of a
+// workgroup is scalar.  Logical framed byte b (= BE32(len) ++ payload ++ 0s)
+// lives in row b / S at b % S (broadcast.rs:174-189); [S, stride) is zeroed.
 __global__ __launch_bounds__(kBlock) void frame_kernel(
-    const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P, size_t count,
+    const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P,
     uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
-    uint32_t k) {
-    const size_t dw_row = shard_stride / 4;
-    const size_t total = count * k * dw_row;
-    for (size_t idx = blockIdx.x * (size_t)kBlock + threadIdx.x; idx < total;
-         idx += (size_t)gridDim.x * kBlock) {
-        const size_t w = idx % dw_row;
-        const size_t row = idx / dw_row;
-        const uint32_t j = (uint32_t)(row % k);
-        const size_t inst = row / k;
-        const uint32_t off = (uint32_t)(4 * w);
-        uint32_t val = 0;
-        if (off < S) {
-            const uint8_t *pay = payloads + inst * payload_stride;
-            const uint64_t lb = (uint64_t)j * S + off;  // logical byte of byte 0
-            const int nvalid = (int)min(4u, S - off);
-            if (lb >= 4) {
-                const uint64_t p0 = lb - 4;
-                if (p0 < P) {
-                    const uint32_t *pw = reinterpret_cast<const uint32_t *>(pay);
-                    const uint64_t a0 = p0 >> 2;
-                    const uint32_t sh = (uint32_t)(p0 & 3) * 8;
-                    uint32_t d0 = pw[a0];
-                    uint32_t d1 = (sh != 0 && 4 * (a0 + 1) < P) ? pw[a0 + 1] : 0u;
-                    uint32_t v = sh ? __builtin_amdgcn_alignbit(d1, d0, sh) : d0;
-                    const uint64_t left = P - p0;
-                    const int nb = (int)min<uint64_t>((uint64_t)nvalid, left);
-                    if (nb < 4) v &= (nb == 0) ? 0u : (0xFFFFFFFFu >> (8 * (4 - nb)));
-                    val = v;
-                }
-            } else {
-                for (int q = 0; q < nvalid; ++q) {
-                    const uint64_t b = lb + q;
-                    uint32_t byte;
-                    if (b < 4)
-                        byte = (P >> (8 * (3 - b))) & 0xFFu;
-                    else
-                        byte = (b - 4 < P) ? pay[b - 4] : 0u;
-                    val |= byte << (8 * q);
-                }
-            }
-        }
-        reinterpret_cast<uint32_t *>(shards + inst * inst_stride + (size_t)j * shard_stride)[w] =
-            val;
+    uint32_t k, uint32_t blocks_per_row) {
+    const uint32_t grow = blockIdx.x / blocks_per_row;  // instance * k + j
+    const uint32_t chunk = (blockIdx.x - grow * blocks_per_row) * kBlock + threadIdx.x;
+    const uint32_t off = chunk * 16;
+    if (off >= shard_stride) return;
+    const size_t inst = grow / k;
+    const uint32_t j = grow - (uint32_t)inst * k;
+    uint4 *dst = reinterpret_cast<uint4 *>(shards + inst * inst_stride + (size_t)j * shard_stride +
+                                           off);
+    if (off >= S) {
+        *dst = make_uint4(0, 0, 0, 0);
+        return;
     }
+    const uint8_t *pay = payloads + inst * payload_stride;
+    const uint64_t lb = (uint64_t)j * S + off;  // logical byte of this chunk's first byte
+    if (lb >= 4 && off + 16 <= S && lb - 4 + 16 <= P) {
+        // every byte is a payload byte: p0 .. p0+15 (all < P, so every dword read is in-row)
+        const uint64_t p0 = lb - 4;
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(pay) + (p0 >> 2);
+        const uint32_t sh = (uint32_t)(p0 & 3) * 8;
+        uint32_t d[5];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = pw[q];
+        d[4] = sh ? pw[4] : 0u;
+        *dst = funnel16(d, sh);
+        return;
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int q = 0; q < 16; ++q) {
+        if (off + q >= S) break;
+        const uint64_t b = lb + q;
+        uint32_t byte;
+        if (b < 4)
+            byte = (P >> (8 * (3 - b))) & 0xFFu;
+        else
+            byte = (b - 4 < P) ? pay[b - 4] : 0u;
+        w[q >> 2] |= byte << (8 * (q & 3));
+    }
+    *dst = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // -------------------------------------------------------------- GF apply --
@@ -88,8 +94,8 @@ template <int RT>
 __global__ __launch_bounds__(kBlock) void gf_apply_kernel(
     uint8_t *__restrict__ base, size_t inst_stride, size_t shard_stride, int n16,
     const uint4 *__restrict__ tables, size_t tab_inst_stride,
-    const uint8_t *__restrict__ in_idx, size_t in_idx_stride,
-    const uint8_t *__restrict__ out_idx, size_t out_idx_stride,
+    const uint32_t *__restrict__ in_idx, size_t in_idx_stride,
+    const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
     const int *__restrict__ nout_arr, int nout_uniform, int nin, int blocks_per_row) {
     const size_t inst = blockIdx.x / blocks_per_row;
     const int chunk0 = (int)(blockIdx.x % blocks_per_row) * kBlock + (int)threadIdx.x;
@@ -99,8 +105,11 @@ __global__ __launch_bounds__(kBlock) void gf_apply_kernel(
     const int nout = nout_arr ? nout_arr[inst] : nout_uniform;
     const int npass = (nout + RT - 1) / RT;
     const uint4 *tab = tables + inst * tab_inst_stride;
-    const uint8_t *iidx = in_idx + inst * in_idx_stride;
-    const uint8_t *oidx = out_idx + inst * out_idx_stride;
+    // 32-bit row indices: wave-uniform, so they come through the scalar cache
+    // (gfx950 has no sub-dword s_load; byte indices became vector loads whose
+    // vmcnt(0) drained the prefetch pipeline)
+    const uint32_t *iidx = in_idx + inst * in_idx_stride;
+    const uint32_t *oidx = out_idx + inst * out_idx_stride;
     const size_t off = (size_t)chunk * 16;
     for (int p = 0; p < npass; ++p) {
         uint32_t acc[RT][4];
@@ -140,6 +149,138 @@ __global__ __launch_bounds__(kBlock) void gf_apply_kernel(
                     const int dst = oidx[p * RT + t];
                     *reinterpret_cast<uint4 *>(ib + (size_t)dst * shard_stride + off) =
                         make_uint4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------- GF bit-sliced ----
+// Bit-sliced GF(2^8) multiply-accumulate.  A lane owns 32 consecutive byte
+// positions of every row; its 8 dwords are transposed into 8 bit-planes
+// (plane b holds bit b of all 32 bytes; three delta-swap stages exchanging
+// the word-index bits with position bits 0..2 -- an involution, so the same
+// three stages transpose back).  c*x = XOR over set bits b of c of
+// (2^b * x); doubling a bit-sliced value is three plane XORs (x^8 = 0x1D),
+// and each set coefficient bit costs 8 full-rate v_xor on 32 positions.
+// Coefficients are wave-uniform scalars, so "bit b of c set" is a scalar
+// branch: about 1 VALU op per byte-MAC against 6 VALU (4 half-rate v_perm)
+// per 4 byte-MACs in gf_apply_kernel.
+__device__ __forceinline__ void bs_transpose(uint32_t (&w)[8]) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int d = 1 << s;
+        const uint32_t m = s == 0 ? 0x55555555u : (s == 1 ? 0x33333333u : 0x0F0F0F0Fu);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i & d) continue;
+            const uint32_t x = w[i], y = w[i | d];
+            const uint32_t t = ((x >> d) ^ y) & m;
+            w[i | d] = y ^ t;
+            w[i] = x ^ (t << d);
+        }
+    }
+}
+
+template <int RT, int MODE>
+// Workgroup = up to 4 waves over the SAME 2048 positions; wave w produces
+// passes w, w + nwaves, ...  The waves read identical input bytes at the
+// same time, so only one copy comes from beyond L1/L2 (a lone wave running
+// its passes one after another re-read every input per pass: 3x the HBM/MALL
+// traffic at m = 42).
+__global__ __launch_bounds__(256) void gf_bitslice_kernel(
+    uint8_t *__restrict__ base, size_t inst_stride, size_t shard_stride, uint32_t row_bytes,
+    const uint8_t *__restrict__ coefs, size_t coef_inst_stride,
+    const uint32_t *__restrict__ in_idx, size_t in_idx_stride,
+    const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
+    const int *__restrict__ nout_arr, int nout_uniform, int nin, uint32_t waves_per_row) {
+    const size_t inst = blockIdx.x / waves_per_row;
+    const int wave = (int)(threadIdx.x >> 6), nwaves = (int)(blockDim.x >> 6);
+    const uint32_t chunk = (blockIdx.x - (uint32_t)inst * waves_per_row) * 64 + (threadIdx.x & 63);
+    uint32_t off = chunk * 32;
+    const bool active = off < row_bytes;
+    if (!active) off = row_bytes - 16;              // clamped, loads stay in the row
+    const bool full = off + 32 <= row_bytes;        // else only 16 bytes belong to this row
+    uint8_t *ib = base + inst * inst_stride;
+    const int nout = nout_arr ? nout_arr[inst] : nout_uniform;
+    const int npass = (nout + RT - 1) / RT;
+    const uint8_t *cf = coefs + inst * coef_inst_stride;
+    // 32-bit row indices: wave-uniform, so they come through the scalar cache
+    // (gfx950 has no sub-dword s_load; byte indices became vector loads whose
+    // vmcnt(0) drained the prefetch pipeline)
+    const uint32_t *iidx = in_idx + inst * in_idx_stride;
+    const uint32_t *oidx = out_idx + inst * out_idx_stride;
+    for (int p = __builtin_amdgcn_readfirstlane(wave); p < npass; p += nwaves) {
+        uint32_t acc[RT][8];
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[t][q] = 0u;
+        // software pipeline, unrolled by two so no register ever moves: the
+        // 32 input bytes of j+1 are in flight (buffer B) while input j
+        // (buffer A) is consumed, and vice versa.  A loop-carried copy would
+        // force s_waitcnt vmcnt(0) at the top of every iteration.
+        const uint4 *cfp = reinterpret_cast<const uint4 *>(cf) + (size_t)p * nin;
+        // Loads are unconditional (index clamped, a half chunk re-reads its own
+        // 16 bytes) so hipcc can count vmcnt exactly instead of draining.
+        auto load_in = [&](int jj, uint4 &l, uint4 &h) {
+            const uint8_t *src = ib + (size_t)iidx[jj < nin ? jj : nin - 1] * shard_stride + off;
+            l = *reinterpret_cast<const uint4 *>(src);
+            h = *reinterpret_cast<const uint4 *>(src + (full ? 16 : 0));
+        };
+        auto consume = [&](int jj, const uint4 &lo, const uint4 &h) {
+            const uint4 hi = full ? h : make_uint4(0, 0, 0, 0);
+            uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            bs_transpose(x);
+            // RT coefficient bytes of input jj for this pass (16-byte padded, scalar load)
+            const uint4 cw = cfp[jj];
+            const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
+            // At step b the planes of 2^b * x sit rotated: logical plane q is
+            // x[(q - b) & 7], so doubling moves no registers, only XORs h into
+            // logical planes 2, 3, 4 (x^8 = x^4 + x^3 + x^2 + 1).
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+#pragma unroll
+                for (int t = 0; t < RT; ++t) {
+                    const uint32_t bit = (c4[t >> 2] >> (8 * (t & 3) + b)) & 1u;
+                    if constexpr (MODE == 2) {
+                        // branch-free: acc ^= x & mask with a wave-uniform mask
+                        const uint32_t mask = 0u - bit;
+#pragma unroll
+                        for (int q = 0; q < 8; ++q)
+                            acc[t][q] ^= x[(q - b) & 7] & mask;  // one v_bitop3
+                    } else if (MODE == 1 ? __builtin_expect(bit, 1) : bit) {
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) acc[t][q] ^= x[(q - b) & 7];
+                    }
+                }
+                if (b < 7) {
+                    const uint32_t h = x[(7 - b) & 7];  // becomes logical plane 0
+                    x[(1 - b) & 7] ^= h;                // -> logical 2
+                    x[(2 - b) & 7] ^= h;                // -> logical 3
+                    x[(3 - b) & 7] ^= h;                // -> logical 4
+                }
+            }
+        };
+        uint4 alo, ahi, blo = make_uint4(0, 0, 0, 0), bhi = make_uint4(0, 0, 0, 0);
+        load_in(0, alo, ahi);
+        for (int j = 0; j < nin; j += 2) {
+            load_in(j + 1, blo, bhi);
+            consume(j, alo, ahi);
+            load_in(j + 2, alo, ahi);
+            if (j + 1 < nin) consume(j + 1, blo, bhi);
+        }
+        if (active) {
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                if (p * RT + t < nout) {
+                    bs_transpose(acc[t]);
+                    uint8_t *dst = ib + (size_t)oidx[p * RT + t] * shard_stride + off;
+                    *reinterpret_cast<uint4 *>(dst) =
+                        make_uint4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+                    if (full)
+                        *reinterpret_cast<uint4 *>(dst + 16) =
+                            make_uint4(acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
                 }
             }
         }
@@ -271,9 +412,9 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(
 // rows equal rse's parity-from-rebuilt-data by linearity over GF(2^8)),
 // expanded to split-2-bit tables for gf_apply_kernel.
 __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
-    int n, int k, int rt, const uint8_t *__restrict__ matrix,
+    int n, int k, int rt, int raw, const uint8_t *__restrict__ matrix,
     const uint8_t *__restrict__ present, uint4 *__restrict__ tables,
-    uint8_t *__restrict__ in_idx, uint8_t *__restrict__ out_idx, int *__restrict__ nout,
+    uint32_t *__restrict__ in_idx, uint32_t *__restrict__ out_idx, int *__restrict__ nout,
     int32_t *__restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *exp_t = smem;             // 512
@@ -379,7 +520,10 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
             const uint8_t *mr = matrix + (size_t)row * k;
             for (int j = 0; j < k; ++j) coef ^= gf_mul_lds(exp_t, log_t, mr[j], aug[j * w2 + k + c]);
         }
-        tab[((size_t)(t / rt) * k + c) * rt + (t % rt)] = gf_split2_entry(coef, exp_t, log_t);
+        if (raw)  // bit-sliced kernel: coefficient bytes [pass][j][16]
+            reinterpret_cast<uint8_t *>(tab)[((size_t)(t / rt) * k + c) * 16 + (t % rt)] = coef;
+        else      // perm kernel: split-2-bit entries [pass][j][rt]
+            tab[((size_t)(t / rt) * k + c) * rt + (t % rt)] = gf_split2_entry(coef, exp_t, log_t);
     }
     for (int j = tid; j < k; j += kBlock) in_idx[inst * (size_t)k + j] = valid[j];
     for (int t = tid; t < nm; t += kBlock) out_idx[inst * (size_t)m + t] = missing[t];
@@ -431,65 +575,166 @@ __global__ __launch_bounds__(kBlock) void decode_check_kernel(
 // --------------------------------------------------------------- unframe --
 // One thread per output dword: logical bytes 4 + 4w .. +3 of the
 // concatenated data rows.
+// One thread per 16 output bytes (payload bytes 16c..16c+15 = logical bytes
+// 4+16c.. of the concatenated data rows, broadcast.rs:590-598); the instance
+// of a workgroup is scalar.  Bytes past the decoded length are written 0.
 __global__ __launch_bounds__(kBlock) void unframe_kernel(
     const uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
-    uint32_t k, size_t count, const uint32_t *__restrict__ plen,
-    const int32_t *__restrict__ status, uint8_t *__restrict__ payload_out,
-    size_t payload_stride) {
+    uint32_t k, const uint32_t *__restrict__ plen, const int32_t *__restrict__ status,
+    uint8_t *__restrict__ payload_out, size_t payload_stride, uint32_t blocks_per_inst) {
+    const size_t inst = blockIdx.x / blocks_per_inst;
+    const uint32_t c = (blockIdx.x - (uint32_t)inst * blocks_per_inst) * kBlock + threadIdx.x;
+    const uint32_t len = plen[inst];
+    const uint32_t o = c * 16;
+    if (status[inst] != 0 || o >= len) return;
     const uint64_t total = (uint64_t)k * S;
-    const size_t dw_inst = total >= 4 ? (size_t)((total - 4 + 3) / 4) : 0;
-    const size_t work = count * dw_inst;
-    for (size_t idx = blockIdx.x * (size_t)kBlock + threadIdx.x; idx < work;
-         idx += (size_t)gridDim.x * kBlock) {
-        const size_t inst = idx / dw_inst;
-        const size_t w = idx - inst * dw_inst;
-        const uint32_t len = plen[inst];
-        if (status[inst] != 0 || 4 * w >= len) continue;
-        const uint8_t *ib = shards + inst * inst_stride;
-        const uint64_t lb = 4 + 4 * (uint64_t)w;
-        const uint32_t row = (uint32_t)(lb / S);
-        const uint32_t off = (uint32_t)(lb - (uint64_t)row * S);
-        uint32_t v;
-        if (off + 4 <= S) {
-            const uint32_t *rw = reinterpret_cast<const uint32_t *>(ib + (size_t)row * shard_stride);
-            const uint32_t a0 = off >> 2, sh = (off & 3) * 8;
-            const uint32_t d0 = rw[a0];
-            v = sh ? __builtin_amdgcn_alignbit(rw[a0 + 1], d0, sh) : d0;
-        } else {
-            v = 0;
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t b = lb + q;
-                if (b < total) v |= (uint32_t)logical_byte(ib, b, S, shard_stride) << (8 * q);
-            }
+    const uint8_t *ib = shards + inst * inst_stride;
+    const uint64_t lb = 4 + (uint64_t)o;
+    const uint32_t row = (uint32_t)(lb / S);
+    const uint32_t off = (uint32_t)(lb - (uint64_t)row * S);
+    uint32_t w[4];
+    if (off + 16 <= S) {
+        // inside one row; the fifth dword ends at most 3 bytes past S (< stride)
+        const uint32_t *rw =
+            reinterpret_cast<const uint32_t *>(ib + (size_t)row * shard_stride) + (off >> 2);
+        const uint32_t sh = (off & 3) * 8;
+        uint32_t d[5];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = rw[q];
+        d[4] = sh ? rw[4] : 0u;
+        const uint4 v = funnel16(d, sh);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+        w[0] = w[1] = w[2] = w[3] = 0;
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t b = lb + q;
+            if (b < total) w[q >> 2] |= (uint32_t)logical_byte(ib, b, S, shard_stride) << (8 * (q & 3));
         }
-        const uint32_t nb = len - 4 * (uint32_t)w;
-        if (nb < 4) v &= 0xFFFFFFFFu >> (8 * (4 - nb));
-        reinterpret_cast<uint32_t *>(payload_out + inst * payload_stride)[w] = v;
+    }
+    const uint32_t nb = len - o;  // bytes of this chunk inside the payload
+    if (nb < 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int keep = (int)nb - 4 * q;
+            if (keep <= 0) w[q] = 0;
+            else if (keep < 4) w[q] &= 0xFFFFFFFFu >> (8 * (4 - keep));
+        }
+    }
+    uint32_t *dst = reinterpret_cast<uint32_t *>(payload_out + inst * payload_stride + o);
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        *reinterpret_cast<uint4 *>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = w[q];
     }
 }
 
 }  // namespace
 
 // ============================================================ launchers ====
+namespace {
+int g_num_cus = 256;
+
+// Residency shaping for the lane-per-sponge kernels.  A sponge cannot be
+// split, so a grid of T sponges runs in ceil(T / resident) rounds and the
+// last round can be mostly idle (cfg3: 524,288 sponges vs 327,680 resident
+// lanes at 5 waves/SIMD = 1.6 rounds, 80 % busy).  Pick the waves/SIMD in
+// [2, max_w] whose rounds are fullest and enforce it with dynamic LDS (one
+// 256-thread block = one wave per SIMD, so blocks/CU = waves/SIMD).
+size_t shaped_lds(size_t lanes, int max_w) {
+    const size_t per_w = (size_t)g_num_cus * kBlock;
+    if (lanes >= per_w * (size_t)max_w * 8) return 0;  // many rounds: the tail is small
+    int best_w = max_w;
+    double best = -1.0;
+    for (int w = max_w; w >= 2; --w) {
+        const size_t cap = per_w * (size_t)w;
+        const size_t rounds = (lanes + cap - 1) / cap;
+        const double util = (double)lanes / (double)(rounds * cap);
+        if (util > best + 1e-9) {
+            best = util;
+            best_w = w;
+        }
+    }
+    if (best_w == max_w) return 0;
+    return (size_t)(163840 / best_w) / 512 * 512;
+}
+constexpr int kSpongeMaxWaves = 5;  // VGPR-limited residency of the sponge kernels (<= 96 VGPRs)
+}  // namespace
+
 hipError_t configure_kernels() {
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(decode_matrix_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    for (const void *k : {reinterpret_cast<const void *>(decode_matrix_kernel),
+                          reinterpret_cast<const void *>(leaf_hash_kernel),
+                          reinterpret_cast<const void *>(validate_kernel)}) {
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
                         size_t count, uint8_t *shards, size_t shard_len, size_t shard_stride,
                         size_t inst_stride, size_t data_shards, hipStream_t s) {
-    const size_t threads = count * data_shards * (shard_stride / 4);
-    if (threads == 0) return hipSuccess;
-    hipLaunchKernelGGL(frame_kernel, dim3(grid_for(threads, 256 * 64)), dim3(kBlock), 0, s,
-                       payloads, payload_stride, (uint32_t)payload_len, count, shards,
-                       (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)data_shards);
+    const size_t chunks = shard_stride / 16;
+    if (count == 0 || chunks == 0) return hipSuccess;
+    const size_t bpr = (chunks + kBlock - 1) / kBlock;
+    const size_t blocks = bpr * count * data_shards;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(frame_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, payloads,
+                       payload_stride, (uint32_t)payload_len, shards, (uint32_t)shard_len,
+                       shard_stride, inst_stride, (uint32_t)data_shards, (uint32_t)bpr);
     return hipGetLastError();
 }
 
 hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     if (a.count == 0 || a.n16 == 0) return hipSuccess;
     if (!a.nout && a.nout_uniform == 0) return hipSuccess;
+    if (a.bitslice) {
+        const uint32_t row_bytes = (uint32_t)a.n16 * 16;
+        const uint32_t wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
+        const size_t blocks = (size_t)wpr * a.count;
+        if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+        const uint8_t *coefs = reinterpret_cast<const uint8_t *>(a.tables);
+        const size_t cstride = a.tab_inst_stride * sizeof(uint4);
+        const int max_rows = a.nout ? a.max_rows : a.nout_uniform;
+        const int nw = std::max(1, std::min(4, (max_rows + a.rt - 1) / a.rt));  // waves per block
+#define HB_BS_CASE(RT)                                                                           \
+    case RT:                                                                                     \
+        if (a.bitslice == 3)                                                                     \
+            hipLaunchKernelGGL((gf_bitslice_kernel<RT, 2>), dim3((unsigned)blocks), dim3(64 * nw), 0, s, \
+                               a.base, a.inst_stride, a.shard_stride, row_bytes, coefs, cstride, \
+                               a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,   \
+                               a.nout_uniform, a.nin, wpr);                                      \
+        else if (a.bitslice == 2)                                                                \
+            hipLaunchKernelGGL((gf_bitslice_kernel<RT, 1>), dim3((unsigned)blocks), dim3(64 * nw), 0, s, \
+                               a.base, a.inst_stride, a.shard_stride, row_bytes, coefs, cstride, \
+                               a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,   \
+                               a.nout_uniform, a.nin, wpr);                                      \
+        else                                                                                     \
+            hipLaunchKernelGGL((gf_bitslice_kernel<RT, 0>), dim3((unsigned)blocks), dim3(64 * nw), 0, s, \
+                               a.base, a.inst_stride, a.shard_stride, row_bytes, coefs, cstride, \
+                               a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,   \
+                               a.nout_uniform, a.nin, wpr);                                      \
+        break
+        switch (a.rt) {
+            HB_BS_CASE(2);
+            HB_BS_CASE(4);
+            HB_BS_CASE(6);
+            HB_BS_CASE(8);
+            HB_BS_CASE(10);
+            HB_BS_CASE(12);
+            HB_BS_CASE(14);
+            HB_BS_CASE(16);
+            default:
+                return hipErrorInvalidValue;
+        }
+#undef HB_BS_CASE
+        return hipGetLastError();
+    }
     const int bpr = (a.n16 + kBlock - 1) / kBlock;
     const size_t blocks = (size_t)bpr * a.count;
 #define HB_GF_CASE(RT)                                                                           \
@@ -528,8 +773,8 @@ hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, size_t shar
                             size_t node_inst_stride, hipStream_t s) {
     const size_t total = n * count;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock), 0,
-                       s, shards, (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)n,
+    hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
+                       shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)n,
                        total, nodes, node_inst_stride);
     return hipGetLastError();
 }
@@ -566,8 +811,8 @@ hipError_t launch_proofs(const uint8_t *nodes, size_t node_inst_stride, size_t n
 hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
     const size_t total = a.count * a.per_inst;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(validate_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock), 0,
-                       s, a.values, (uint32_t)a.value_len, a.value_stride, a.value_inst_stride,
+    hipLaunchKernelGGL(validate_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
+                       shaped_lds(total, kSpongeMaxWaves), s, a.values, (uint32_t)a.value_len, a.value_stride, a.value_inst_stride,
                        (uint32_t)a.per_inst, a.indices, a.digests, (uint32_t)a.dslots, a.ndig,
                        a.roots, a.root_stride, (uint32_t)a.tree_n, a.count, a.ok_out);
     return hipGetLastError();
@@ -577,7 +822,7 @@ hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
     hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(kBlock), lds, s, a.n,
-                       a.k, a.rt, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
+                       a.k, a.rt, a.raw, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
     return hipGetLastError();
 }
 
@@ -600,11 +845,14 @@ hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, size_t shard_
                           const uint32_t *plen, const int32_t *status, uint8_t *payload_out,
                           size_t payload_stride, hipStream_t s) {
     const uint64_t total = (uint64_t)data_shards * shard_len;
-    if (count == 0 || total < 4) return hipSuccess;
-    const size_t threads = count * (size_t)((total - 4 + 3) / 4);
-    hipLaunchKernelGGL(unframe_kernel, dim3(grid_for(threads, 256 * 64)), dim3(kBlock), 0, s,
-                       shards, (uint32_t)shard_len, shard_stride, inst_stride,
-                       (uint32_t)data_shards, count, plen, status, payload_out, payload_stride);
+    if (count == 0 || total <= 4) return hipSuccess;  // nothing past the length prefix
+    const size_t chunks = (size_t)((total - 4 + 15) / 16);
+    const size_t bpi = (chunks + kBlock - 1) / kBlock;
+    const size_t blocks = bpi * count;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(unframe_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, shards,
+                       (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)data_shards,
+                       plen, status, payload_out, payload_stride, (uint32_t)bpi);
     return hipGetLastError();
 }
 

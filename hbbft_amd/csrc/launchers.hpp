@@ -21,14 +21,16 @@ struct GfApplyArgs {
     int n16;                    // 16-byte chunks per row
     const uint4 *tables;        // split-2-bit entries [inst][pass][nin][rt]
     size_t tab_inst_stride;     // in entries (0: shared)
-    const uint8_t *in_idx;      // [inst][nin]
+    const uint32_t *in_idx;     // [inst][nin]
     size_t in_idx_stride;       // 0: shared
-    const uint8_t *out_idx;     // [inst][max_out]
+    const uint32_t *out_idx;    // [inst][max_out]
     size_t out_idx_stride;      // 0: shared
     const int *nout;            // [inst] or nullptr
     int nout_uniform;
+    int max_rows;               // upper bound of nout[] (per-instance row counts)
     int nin;
     int rt;                     // rows per pass: one of 2,4,...,16
+    int bitslice;               // 1: gf_bitslice_kernel, tables = coefficient bytes [pass][nin][16]
     size_t count;
 };
 // Row tile for `rows` output rows: fewest passes of <= 16, evened out.
@@ -65,13 +67,13 @@ hipError_t launch_validate(const ValidateArgs &a, hipStream_t s);
 // Per-instance decode matrix: inv(M[first k present]) applied to
 // M[missing rows] -> split-2-bit tables + row index lists.
 struct DecodeMatrixArgs {
-    int n, k, rt;
+    int n, k, rt, raw;          // raw: coefficient bytes for the bit-sliced kernel
     const uint8_t *matrix;      // n x k encoding matrix (device)
     const uint8_t *present;     // [count][n]
     size_t count;
     uint4 *tables;              // [count][ceil(m/rt)][k][rt]
-    uint8_t *in_idx;            // [count][k]
-    uint8_t *out_idx;           // [count][m]
+    uint32_t *in_idx;           // [count][k]
+    uint32_t *out_idx;          // [count][m]
     int *nout;                  // [count]
     int32_t *status;            // [count]
 };

@@ -175,8 +175,9 @@ int hbrbc_reconstruct_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len,
                             size_t count, int32_t *status_out, void *stream);
 /* decode_from_shards (broadcast.rs:563-601): reconstruct, re-tree over all n
  * shards, compare with roots[i*root_stride..+32], unframe.  payload bytes of
- * instance i go to payload_out + i*payload_stride (payload_stride >=
- * data*shard_len rounded up to 4), their length to payload_len_out[i] and
+ * instance i go to payload_out + i*payload_stride (payload_stride a multiple
+ * of 4 and >= round_up(data*shard_len - 4, 16); every instance's row must
+ * hold that many bytes, bytes past the payload are written 0), their length to payload_len_out[i] and
  * the outcome to status_out[i] (OK, TOO_FEW_SHARDS_PRESENT, ROOT_MISMATCH,
  * NO_PAYLOAD_LEN).  `nodes` (count x node_inst_stride) receives the
  * re-built trees. */
