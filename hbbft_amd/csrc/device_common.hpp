@@ -122,15 +122,26 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     for (int i = 0; i < 25; ++i) L[i] = H[i] = 0u;
     const uint2 *q = reinterpret_cast<const uint2 *>(p);
     const uint32_t nfull = len / 136u;
-    for (uint32_t t = 0; t < nfull; ++t) {
+    // Full blocks, software-pipelined: block t+1 is loaded while block t is
+    // permuted, so the sponge never waits on memory between permutations
+    // (+34 VGPRs; the sponge kernels run at 4 waves/SIMD either way).
+    if (nfull) {
+        uint2 nx[17];
 #pragma unroll
-        for (int w = 0; w < 17; ++w) {
-            const uint2 v = q[w];
-            L[w] ^= v.x;
-            H[w] ^= v.y;
+        for (int w = 0; w < 17; ++w) nx[w] = q[w];
+        for (uint32_t t = 0; t < nfull; ++t) {
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                L[w] ^= nx[w].x;
+                H[w] ^= nx[w].y;
+            }
+            q += 17;
+            if (t + 1 < nfull) {
+#pragma unroll
+                for (int w = 0; w < 17; ++w) nx[w] = q[w];
+            }
+            keccak_f1600(L, H);
         }
-        q += 17;
-        keccak_f1600(L, H);
     }
     // last (partial) block + pad10*1 with the SHA3 domain byte 0x06
     const int r = (int)(len - nfull * 136u);

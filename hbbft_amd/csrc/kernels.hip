@@ -35,6 +35,42 @@ __device__ __forceinline__ uint4 funnel16(const uint32_t (&d)[5], uint32_t sh) {
                       __builtin_amdgcn_alignbit(d[4], d[3], sh));
 }
 
+// Bytes [SH, SH + 16) of the 32-byte little-endian window (a, b): four
+// v_alignbyte_b32, or plain moves when SH is a multiple of 4.
+template <int SH>
+__device__ __forceinline__ uint4 window16(const uint4 &a, const uint4 &b) {
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    constexpr int ws = SH >> 2, bs = SH & 3;
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if constexpr (bs == 0)
+            o[i] = w[i + ws];
+        else
+            o[i] = __builtin_amdgcn_alignbyte(w[i + ws + 1], w[i + ws], bs);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// 16 bytes starting `sh` bytes into the 16-byte aligned `src`, from one or two
+// coalesced 16-byte loads.  `sh` must be wave-uniform (the switch is scalar)
+// and src + 32 readable when sh != 0.
+__device__ __forceinline__ uint4 load16_shifted(const uint8_t *src, uint32_t sh) {
+    const uint4 a = *reinterpret_cast<const uint4 *>(src);
+    if (sh == 0) return a;
+    const uint4 b = *reinterpret_cast<const uint4 *>(src + 16);
+    switch (sh) {
+#define HB_W16(s) \
+    case s:       \
+        return window16<s>(a, b);
+        HB_W16(1) HB_W16(2) HB_W16(3) HB_W16(4) HB_W16(5) HB_W16(6) HB_W16(7) HB_W16(8)
+        HB_W16(9) HB_W16(10) HB_W16(11) HB_W16(12) HB_W16(13) HB_W16(14)
+#undef HB_W16
+        default:
+            return window16<15>(a, b);
+    }
+}
+
 // One thread per 16-byte chunk of every data row; the (instance, row) of a
 // workgroup is scalar.  Logical framed byte b (= BE32(len) ++ payload ++ 0s)
 // lives in row b / S at b % S (broadcast.rs:174-189); [S, stride) is zeroed.
@@ -56,7 +92,23 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(
     }
     const uint8_t *pay = payloads + inst * payload_stride;
     const uint64_t lb = (uint64_t)j * S + off;  // logical byte of this chunk's first byte
-    if (lb >= 4 && off + 16 <= S && lb - 4 + 16 <= P) {
+    const bool interior = lb >= 4 && off + 16 <= S && lb - 4 + 16 <= P;
+    // Interior chunks of one row share a source misalignment.  When the whole
+    // wave agrees, read the payload with aligned 16-byte loads (coalesced) and
+    // shift in registers; the aligned window must stay inside the payload row.
+    {
+        const uintptr_t row0 = reinterpret_cast<uintptr_t>(pay);
+        const uintptr_t src = row0 + (interior ? lb - 4 : 0);
+        const uint32_t sh = (uint32_t)(src & 15);
+        const uintptr_t a0 = src - sh;
+        const bool fits = interior && a0 >= row0 && a0 + (sh ? 32 : 16) <= row0 + payload_stride;
+        const uint32_t sh0 = __builtin_amdgcn_readfirstlane(sh);
+        if (__all(fits && sh == sh0)) {
+            *dst = load16_shifted(reinterpret_cast<const uint8_t *>(a0), sh0);
+            return;
+        }
+    }
+    if (interior) {
         // every byte is a payload byte: p0 .. p0+15 (all < P, so every dword read is in-row)
         const uint64_t p0 = lb - 4;
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(pay) + (p0 >> 2);
@@ -593,7 +645,15 @@ __global__ __launch_bounds__(kBlock) void unframe_kernel(
     const uint32_t row = (uint32_t)(lb / S);
     const uint32_t off = (uint32_t)(lb - (uint64_t)row * S);
     uint32_t w[4];
-    if (off + 16 <= S) {
+    // Chunks inside one row share a misalignment: when the wave agrees, two
+    // aligned 16-byte loads (coalesced) and a register shift.  off + 16 <= S
+    // <= stride keeps the second 16 bytes inside the row when sh != 0.
+    const uint32_t sh = off & 15u;
+    const uint32_t sh0 = __builtin_amdgcn_readfirstlane(sh);
+    if (__all(off + 16 <= S && sh == sh0)) {
+        const uint4 v = load16_shifted(ib + (size_t)row * shard_stride + (off - sh), sh0);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else if (off + 16 <= S) {
         // inside one row; the fifth dword ends at most 3 bytes past S (< stride)
         const uint32_t *rw =
             reinterpret_cast<const uint32_t *>(ib + (size_t)row * shard_stride) + (off >> 2);
@@ -658,7 +718,7 @@ size_t shaped_lds(size_t lanes, int max_w) {
     if (best_w == max_w) return 0;
     return (size_t)(163840 / best_w) / 512 * 512;
 }
-constexpr int kSpongeMaxWaves = 5;  // VGPR-limited residency of the sponge kernels (<= 96 VGPRs)
+constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kernels (<= 128 VGPRs)
 }  // namespace
 
 hipError_t configure_kernels() {

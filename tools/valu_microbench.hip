@@ -46,6 +46,13 @@ __global__ __launch_bounds__(256) void op_loop(uint32_t *out, int iters, uint32_
                 if constexpr (KIND == 9) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a[i]));
                 if constexpr (KIND == 10) asm volatile("v_alignbyte_b32 %0, %0, %1, 1" : "+v"(a[i]) : "v"(b));
                 if constexpr (KIND == 11) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+                // 64-bit shifts: one instruction moves a whole (lo, hi) lane pair
+                if constexpr (KIND == 12)
+                    asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(*(uint64_t *)&a[i & 14]));
+                if constexpr (KIND == 13)
+                    asm volatile("v_lshl_add_u64 %0, %0, 7, %1" : "+v"(*(uint64_t *)&a[i & 14]) : "v"(*(uint64_t *)&a[(i + 2) & 14]));
+                if constexpr (KIND == 14) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(a[i]));
+                if constexpr (KIND == 15) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
             }
         }
     }
@@ -94,13 +101,14 @@ int main() {
     const int blocks = cus * 8 * 16;  // many full rounds of residency
     CHECK(hipMalloc(&out, (size_t)blocks * 256 * 4));
     const int iters = 64;
-    const char *names[12] = {"v_xor_b32", "v_bitop3_b32", "v_alignbit_b32(v,v)", "v_perm_b32(s,s,v)",
+    const char *names[16] = {"v_xor_b32", "v_bitop3_b32", "v_alignbit_b32(v,v)", "v_perm_b32(s,s,v)",
                              "v_and_b32", "v_lshl_or_b32", "v_alignbit_b32(s,v)", "v_perm_b32(v,v,v)",
-                             "v_pk_mov_b32", "v_lshrrev_b32", "v_alignbyte_b32", "v_add_u32"};
+                             "v_pk_mov_b32", "v_lshrrev_b32", "v_alignbyte_b32", "v_add_u32",
+                             "v_lshrrev_b64", "v_lshl_add_u64", "v_lshlrev_b32", "v_or3_b32"};
 #define K(n) case n: hipLaunchKernelGGL(op_loop<n>, dim3(blocks), dim3(256), 0, 0, out, iters, 1u); break
-    for (int kind = 0; kind < 12; ++kind) {
+    for (int kind = 0; kind < 16; ++kind) {
         float ms = time_ms([&] {
-            switch (kind) { K(0); K(1); K(2); K(3); K(4); K(5); K(6); K(7); K(8); K(9); K(10); K(11); }
+            switch (kind) { K(0); K(1); K(2); K(3); K(4); K(5); K(6); K(7); K(8); K(9); K(10); K(11); K(12); K(13); K(14); K(15); }
         });
         const double instr = (double)blocks * 256 * iters * 8 * 16;
         printf("%-22s %8.3f ms  %6.2f T lane-instr/s\n", names[kind], ms, instr / ms / 1e9);
