@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-batches per step, each on its own HIP stream (overlap)")
+    ap.add_argument("--mode", choices=["instances", "validators"], default=None,
+                    help="instances: every rank runs whole instances, no collective (default "
+                         "except cfg4); validators: simulated validators sharded over the ranks, "
+                         "Value/Echo exchanged by all-to-all (hbbft_amd/sharded.py; default for cfg4)")
     return ap.parse_args()
 
 
@@ -69,6 +73,9 @@ def main():
     n, plen, count, erase = CONFIGS[args.config]
     if args.count:
         count = args.count
+    mode = args.mode or ("validators" if args.config == "cfg4" else "instances")
+    if mode == "validators":
+        return run_validators(args, n, plen, count, rank, world, local, dev)
     nsub = max(1, min(args.streams, count))
     f = (n - 1) // 3
     # one Coding context per sub-batch: each owns its reconstruct workspace
@@ -252,6 +259,117 @@ def main():
                        "streams_per_gpu": nsub},
             "roofline": roofline, "cpu_baseline": cpu,
             "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_validators(args, n, plen, count, rank, world, local, dev):
+    """Validator-sharded simulation: each rank proposes `count`
+    instances and hosts N/world validators; Value and Echo rows cross ranks
+    in two all-to-alls (RCCL over xGMI), roots in an all-gather."""
+    import torch
+    import torch.distributed as dist
+
+    from hbbft_amd.sharded import DistExchange, ShardedBroadcast, SoloExchange
+
+    sb = ShardedBroadcast(n, count, plen, rank, world, device=local)
+    ex = DistExchange() if world > 1 else SoloExchange()
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x48424246 + rank)
+    pstride = (plen + 15) // 16 * 16
+    payloads = torch.randint(0, 256, (count, pstride), dtype=torch.uint8, device=dev, generator=g)
+    xev = []   # (start, end) events around the two exchanges, on torch's stream
+
+    def step(timed=False):
+        sb.propose(payloads)
+        sb.pack_value()
+        a = torch.cuda.Event(enable_timing=True) if timed else None
+        if a:
+            a.record()
+        sb.exchange_value(ex)
+        if a:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            xev.append((a, b))
+        sb.validate_values()
+        a = torch.cuda.Event(enable_timing=True) if timed else None
+        if a:
+            a.record()
+        sb.exchange_echo(ex)
+        if a:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            xev.append((a, b))
+        sb.decode()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if not args.no_verify:
+        real = len(sb.topo.validators(rank))
+        assert bool((sb.ok_v[:, :, :real] == 1).all()), "a valid Value proof was rejected"
+        assert bool((sb.status == 0).all()), "decode failed"
+        assert bool((sb.plen_out == plen).all())
+        assert torch.equal(sb.out[:, :plen], payloads[:, :plen]), "decoded payload differs"
+    sb.rb.profile(True)
+    sb.rb.profile_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    sb.rb.profile(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    stages = {k: v for k, v in sb.rb.profile_read().items()}
+    xms = sum(a.elapsed_time(b) for a, b in xev)
+    S, k, m = sb.S, sb.rb.k, sb.rb.m
+    L = (S + 1 + 135) // 136
+    alg_bytes = {"frame": plen + k * S, "encode": (k + m) * S, "leaf_hash": n * (S + 32),
+                 "validate": n * (S + 32 * (sb.rb.dslots + 1) + 1), "reconstruct": (k + sb.topo.f) * S,
+                 "unframe": k * S + plen}
+    dom = max(alg_bytes, key=lambda s_: stages[s_][0])
+    dom_ms, dom_launches = stages[dom]
+    per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
+    achieved = alg_bytes[dom] * count / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    perms = {"leaf_hash": count * n * L, "validate": count * (n * L + n * sb.rb.dslots)}
+    valu = None
+    if dom in perms:
+        ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
+        valu = {"achieved_ops": ops, "peak_ops": VALU_PEAK_OPS, "frac": ops / VALU_PEAK_OPS,
+                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom]}
+    xbytes = 2 * (world - 1) / world * count * sb.topo.npad * sb.stride
+    value = float(count) * plen * world * args.steps / elapsed / 1e9
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (uniform random payloads resident in HBM)",
+            "config": {"workload": "%s: N=%d f=%d (%d+%d shards), %d B payloads, %d proposals/GPU, "
+                                   "validators sharded over %d GPUs (%d each), Value + Echo "
+                                   "all-to-all, receiver misses its f right-hand Echoes"
+                                   % (args.config, n, sb.topo.f, k, m, plen, count, world,
+                                      sb.topo.rpg),
+                       "n": n, "f": sb.topo.f, "payload_bytes": plen, "shard_len": S,
+                       "instances_per_gpu": count, "global_batch": count * world,
+                       "parallelism": "validator-sharded x%d" % world},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "launch_ms": per_launch_s * 1e3, "valu": valu},
+            "exchange": {"ms_per_step": xms / args.steps, "bytes_per_step_per_gpu": xbytes,
+                         "GBps_per_gpu": xbytes / (xms / args.steps / 1e3) / 1e9 if xms else None},
+            "cpu_baseline": None,
+            "stages_ms_per_step": {s_: stages[s_][0] / args.steps for s_ in stages},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -400,6 +400,21 @@ class RbcBatch:
                                           _ptr(ndig), _ptr(root), nodes.stride(0), self.n,
                                           count, _ptr(ok), self._stream(stream)))
 
+    def validate_rows(self, values, S, per_inst, indices, digests, ndig, roots, ok, stream=None):
+        """Proof::validate for proofs laid out as [count][per_inst] rows: values
+        uint8 [count, per_inst, >=S] (any row/instance stride that is a multiple of
+        8), indices int32 [count, per_inst] (the index each proof claims and
+        the receiver expects), digests uint8 [count, per_inst, dslots, 32],
+        ndig uint8 [count, per_inst], roots uint8 [count, >=32], ok uint8
+        [count, per_inst].  Trees have self.n leaves."""
+        count = values.shape[0]
+        for t in (indices, digests, ndig, ok):
+            assert t.is_contiguous() and t.shape[0] == count and t.shape[1] == per_inst
+        _check(lib().hbrbc_validate_batch(self.coding.handle, _ptr(values), S, values.stride(1),
+                                          values.stride(0), per_inst, _ptr(indices), _ptr(digests),
+                                          _ptr(ndig), _ptr(roots), roots.stride(0), self.n, count,
+                                          _ptr(ok), self._stream(stream)))
+
     def reconstruct(self, slab, S, present, status, stream=None):
         _check(lib().hbrbc_reconstruct_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
                                              slab.stride(0), _ptr(present), slab.shape[0],
