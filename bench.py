@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=1,
                     help="sub-batches per step, each on its own HIP stream (overlap)")
     ap.add_argument("--mode", choices=["instances", "validators"], default=None,
                     help="instances: every rank runs whole instances, no collective (default "

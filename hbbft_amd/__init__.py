@@ -16,6 +16,7 @@ import os
 __all__ = [
     "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
     "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
+    "jit_build_encode",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -91,6 +92,8 @@ def lib():
         "hbrbc_profile_reset": (ctypes.c_int, [_P]),
         "hbrbc_profile_read": (ctypes.c_int, [_P, _P, _P]),
         "hbrbc_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
+        "hbrbc_encode_kernel": (ctypes.c_char_p, [_P]),
+        "hbrbc_jit_build_encode": (ctypes.c_int, [_S, _S, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -103,6 +106,13 @@ def lib():
 def _check(code):
     if code != 0:
         raise RseError(code, lib().hbrbc_last_error().decode(errors="replace"))
+
+
+def jit_build_encode(data_shards, parity_shards, directory=None):
+    """Generate + compile (hiprtc, gfx950; no GPU needed) the specialised RS
+    encoder for this matrix into the code-object cache (jit.hip)."""
+    _check(lib().hbrbc_jit_build_encode(data_shards, parity_shards,
+                                        directory.encode() if directory else None))
 
 
 def shard_len(payload_len, data_shards):
@@ -176,6 +186,10 @@ class Coding:
 
     def data_shard_count(self):
         return lib().hbrbc_data_shard_count(self._h)
+
+    def encode_kernel(self):
+        """Which encode kernel this context runs: specialised / bitslice / perm / trivial."""
+        return lib().hbrbc_encode_kernel(self._h).decode()
 
     def parity_shard_count(self):
         return lib().hbrbc_parity_shard_count(self._h)

@@ -16,8 +16,12 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+#include <sys/stat.h>
+
 #include "../../include/hbrbc.h"
 #include "device_common.hpp"
+#include "jit.hpp"
 #include "launchers.hpp"
 
 using namespace hbrbc;
@@ -160,6 +164,12 @@ struct hbrbc_ctx {
     int bitslice = 1;            // GF kernel: 1 bit-sliced (default), 0 split-2-bit v_perm
     std::vector<uint8_t> matrix;  // n x k
     hipStream_t stream = nullptr;
+    // specialised encoder (jit.hip) for this matrix, when its code object is available
+    hipModule_t enc_mod = nullptr;
+    hipFunction_t enc_fn = nullptr;
+    int rt_spec = 2;              // parity rows per pass of the specialised encoder
+    int depth_spec = 4;           // its data-row prefetch depth
+    std::string enc_kind = "none";
     DevBuf d_matrix, d_enc_tables, d_enc_in, d_enc_out;
     // reconstruct workspace
     size_t ws_count = 0;
@@ -325,6 +335,87 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shar
     return HBRBC_OK;
 }
 
+// Directory of cached specialised-encoder code objects: $HBRBC_JIT_DIR, else
+// <directory of libhbrbc.so>/jit.
+std::string jit_dir() {
+    if (const char *e = getenv("HBRBC_JIT_DIR")) return e;
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void *>(&hbrbc_version), &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        const size_t cut = p.find_last_of('/');
+        return (cut == std::string::npos ? std::string(".") : p.substr(0, cut)) + "/jit";
+    }
+    return "jit";
+}
+
+std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth) {
+    return dir + "/" + encode_kernel_name(k, m, rt, depth) + "_v3.co";
+}
+
+// Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).
+int spec_depth() {
+    if (const char *e = getenv("HBRBC_JIT_DEPTH")) return std::max(1, std::min(8, atoi(e)));
+    return 4;
+}
+
+bool read_file(const std::string &path, std::vector<char> &out) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n > 0 && fread(out.data(), 1, out.size(), f) == out.size();
+    fclose(f);
+    return ok;
+}
+
+// Parity rows per pass of the specialised encoder: the accumulators (8 VGPRs
+// per row) plus the planes, pair XORs and load buffers must stay near 200
+// VGPRs (2 waves/SIMD) without spilling.
+int spec_row_tile(size_t m) {
+    if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(16, atoi(e) & ~1));
+    return gf_row_tile((int)m);
+}
+
+// Load (or, with HBRBC_JIT=1, compile and cache) the specialised encoder.
+// Any failure leaves the context on the generic bit-sliced kernel.
+void setup_spec_encoder(hbrbc_ctx *c) {
+    const char *mode = getenv("HBRBC_JIT");
+    if (c->m == 0 || (mode && !std::strcmp(mode, "0")) || c->k * c->m > 8192) return;
+    c->rt_spec = spec_row_tile(c->m);
+    c->depth_spec = spec_depth();
+    const std::string path = jit_file(jit_dir(), c->k, c->m, c->rt_spec, c->depth_spec);
+    std::vector<char> code;
+    if (!read_file(path, code)) {
+        if (!mode || std::strcmp(mode, "1")) return;
+        std::string log;
+        if (compile_encode(c->k, c->m, c->matrix.data() + c->k * c->k, c->rt_spec, c->depth_spec,
+                           code, log)) {
+            c->enc_kind = "jit-failed";
+            return;
+        }
+        mkdir(jit_dir().c_str(), 0755);
+        if (FILE *f = fopen(path.c_str(), "wb")) {
+            fwrite(code.data(), 1, code.size(), f);
+            fclose(f);
+        }
+    }
+    if (hipModuleLoadData(&c->enc_mod, code.data()) != hipSuccess) {
+        c->enc_mod = nullptr;
+        return;
+    }
+    if (hipModuleGetFunction(&c->enc_fn, c->enc_mod,
+                             encode_kernel_name(c->k, c->m, c->rt_spec, c->depth_spec).c_str()) !=
+        hipSuccess) {
+        (void)hipModuleUnload(c->enc_mod);
+        c->enc_mod = nullptr;
+        c->enc_fn = nullptr;
+        return;
+    }
+    c->enc_kind = "specialised";
+}
+
 std::once_flag g_default_once;
 hbrbc_ctx *g_default = nullptr;
 int g_default_status = HBRBC_OK;
@@ -429,6 +520,8 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
         hbrbc_coding_free(c);
         return st;
     }
+    c->enc_kind = c->m == 0 ? "trivial" : (c->bitslice ? "bitslice" : "perm");
+    if (c->bitslice) setup_spec_encoder(c);
     *out = c;
     return HBRBC_OK;
 }
@@ -443,6 +536,7 @@ void hbrbc_coding_free(hbrbc_ctx *c) {
                       &c->st_aux3})
         b->release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->enc_mod) (void)hipModuleUnload(c->enc_mod);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -514,6 +608,21 @@ int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     HB_HIP(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     StageTimer t(c, HBRBC_STAGE_ENCODE, s);
+    if (c->enc_fn) {
+        // specialised XOR network (jit.hip): same lane mapping as the bit-sliced kernel
+        uint8_t *base = shards;
+        unsigned long ist = inst_stride, sst = shard_stride;
+        unsigned row_bytes = (unsigned)(round_up(shard_len, 16));
+        unsigned wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
+        const size_t blocks = (size_t)wpr * count;
+        if (blocks > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "grid too large");
+        const int npass = (int)((c->m + c->rt_spec - 1) / c->rt_spec);
+        const unsigned threads = 64u * (unsigned)std::min(4, npass);
+        void *args[] = {&base, &ist, &sst, &row_bytes, &wpr};
+        HB_HIP(hipModuleLaunchKernel(c->enc_fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args,
+                                     nullptr));
+        return HBRBC_OK;
+    }
     GfApplyArgs g;
     g.base = shards;
     g.inst_stride = inst_stride;
@@ -867,6 +976,31 @@ int hbrbc_proof_validate(const uint8_t *value, size_t len, size_t index, const u
     HB_HIP(hipStreamSynchronize(c->stream));
     *valid_out = ok ? 1 : 0;
     return HBRBC_OK;
+}
+
+// ------------------------------------------------------ specialised encode --
+const char *hbrbc_encode_kernel(const hbrbc_ctx *c) { return c ? c->enc_kind.c_str() : "none"; }
+
+int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char *dir) {
+    if (data_shards == 0 || parity_shards == 0 || data_shards + parity_shards > 256)
+        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, data + parity <= 256");
+    std::vector<uint8_t> mat;
+    if (!build_matrix(data_shards, data_shards + parity_shards, mat))
+        return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
+    const int rt = spec_row_tile(parity_shards), depth = spec_depth();
+    std::vector<char> code;
+    std::string log;
+    if (compile_encode(data_shards, parity_shards, mat.data() + data_shards * data_shards, rt,
+                       depth, code, log))
+        return fail(HBRBC_E_DEVICE, "hiprtc: %s", log.substr(0, 400).c_str());
+    const std::string d = dir ? std::string(dir) : jit_dir();
+    mkdir(d.c_str(), 0755);
+    const std::string path = jit_file(d, data_shards, parity_shards, rt, depth);
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f) return fail(HBRBC_E_INVALID_ARG, "cannot write %s", path.c_str());
+    const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+    fclose(f);
+    return ok ? HBRBC_OK : fail(HBRBC_E_INVALID_ARG, "short write %s", path.c_str());
 }
 
 // ------------------------------------------------------------- profiling --

@@ -145,13 +145,17 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     }
     // last (partial) block + pad10*1 with the SHA3 domain byte 0x06
     const int r = (int)(len - nfull * 136u);
+    // issue every tail load before the first use: one memory wait for the
+    // block instead of one per 8-byte word
+    uint2 tl[17];
+#pragma unroll
+    for (int w = 0; w < 17; ++w) tl[w] = (r - 8 * w > 0) ? q[w] : make_uint2(0u, 0u);
 #pragma unroll
     for (int w = 0; w < 17; ++w) {
         const int rem = r - 8 * w;
         uint64_t v = 0;
         if (rem > 0) {
-            const uint2 x = q[w];
-            v = ((uint64_t)x.y << 32) | x.x;
+            v = ((uint64_t)tl[w].y << 32) | tl[w].x;
             if (rem < 8) v &= ~0ull >> (64 - 8 * rem);
         }
         if (rem >= 0 && rem < 8) v ^= 0x06ull << (8 * rem);

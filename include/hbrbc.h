@@ -189,6 +189,19 @@ int hbrbc_decode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t
 /* Pre-size the reconstruct workspace for `count` instances. */
 int hbrbc_reserve(hbrbc_ctx *ctx, size_t count);
 
+/* ---- specialised encoder ------------------------------------------------ */
+/* Coding::encode runs either the generic bit-sliced GF kernel or, when a code
+ * object for this (data, parity) matrix is cached under <lib dir>/jit (or
+ * $HBRBC_JIT_DIR), a kernel generated for the matrix: a fixed XOR network on
+ * bit planes (hbbft_amd/csrc/jit.hip), bit-identical output.  Returns
+ * "specialised", "bitslice", "perm", "trivial" or "jit-failed". */
+const char *hbrbc_encode_kernel(const hbrbc_ctx *ctx);
+/* Generate and compile (hiprtc, gfx950, no device needed) the specialised
+ * encoder for rse build_matrix(data, data + parity) into `dir` (NULL: the
+ * default directory).  With HBRBC_JIT=1 a context compiles a missing one
+ * itself; HBRBC_JIT=0 disables the specialised path. */
+int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char *dir);
+
 /* ---- measurement hooks (bench.py) --------------------------------------- */
 /* Stage ids for the per-stage device timers. */
 enum hbrbc_stage {

@@ -113,16 +113,20 @@ int main() {
         const double instr = (double)blocks * 256 * iters * 8 * 16;
         printf("%-22s %8.3f ms  %6.2f T lane-instr/s\n", names[kind], ms, instr / ms / 1e9);
     }
-    const int kblocks = cus * 5 * 4;  // exactly one residency round at 5 waves/SIMD
-    for (int rounds : {1, 4}) {
-        const int nb = kblocks * rounds;
+    // residency forced with dynamic LDS: one 256-thread block = one wave per
+    // SIMD, so w blocks per CU = w waves per SIMD
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(keccak_loop),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (int w : {2, 3, 4, 5}) {
+        const size_t lds = (size_t)(163840 / w) / 512 * 512;
+        const int nb = cus * w * 4;  // four full residency rounds
         const int kit = 64;
         float ms = time_ms([&] {
-            hipLaunchKernelGGL(keccak_loop, dim3(nb), dim3(256), 0, 0, out, kit);
+            hipLaunchKernelGGL(keccak_loop, dim3(nb), dim3(256), lds, 0, out, kit);
         });
         const double perms = (double)nb * 256 * kit;
-        printf("keccak-f1600 x%d rounds of residency: %8.3f ms  %.3f G perm/s  = %.2f T ops/s @4320 "
-               "ops/perm\n", rounds, ms, perms / ms / 1e6, perms * 4320 / ms / 1e9);
+        printf("keccak-f1600 at %d waves/SIMD: %8.3f ms  %.3f G perm/s  = %.2f T ops/s @4320 "
+               "ops/perm\n", w, ms, perms / ms / 1e6, perms * 4320 / ms / 1e9);
     }
     return 0;
 }
