@@ -220,7 +220,7 @@ def main():
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
-            pm = json.load(open(prof))
+            pm = json.load(open(prof)).get("traffic", {})
             key = "%s:%s" % (args.config, dom)
             if key in pm:   # HBM bytes per instance from the PMC pass x instances per launch
                 roofline["traffic"] = pm[key] * per_launch
