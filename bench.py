@@ -28,7 +28,7 @@ KECCAK_OPS_PER_PERM = 4320     # ~180 VALU ops/round x 24 rounds
 CONFIGS = {
     # name: (N, payload bytes, instances per GPU, erasures)
     "cfg2": (16, 1 << 20, 4096, "f"),
-    "cfg3": (64, 256 << 10, 8192, "f"),
+    "cfg3": (64, 256 << 10, 16384, "f"),
     "cfg4": (128, 256 << 10, 8192, "f"),
     "cfg5": (250, 4 << 20, 1024, "worst"),
 }
