@@ -16,7 +16,7 @@ import os
 __all__ = [
     "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
     "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
-    "jit_build_encode",
+    "jit_build_encode", "WIRE_VARIANTS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -28,8 +28,10 @@ STATUS_NAMES = {
     7: "TooFewBufferShards", 8: "TooManyBufferShards", 9: "IncorrectShardSize",
     10: "TooFewShardsPresent", 11: "EmptyShard", 12: "InvalidShardFlags", 13: "InvalidIndex",
     64: "SingularMatrix", 65: "RootMismatch", 66: "NoPayloadLen",
+    70: "WireTruncated", 71: "WireBadVariant", 72: "WireTooLarge",
     100: "InvalidArgument", 101: "DeviceError", 102: "NoDevice",
 }
+WIRE_VARIANTS = {"Value": 0, "Echo": 1, "Ready": 2, "CanDecode": 3, "EchoHash": 4}
 STAGES = ["frame", "encode", "leaf_hash", "tree_levels", "proofs", "validate",
           "decode_matrix", "reconstruct", "unframe"]
 
@@ -93,6 +95,11 @@ def lib():
         "hbrbc_profile_read": (ctypes.c_int, [_P, _P, _P]),
         "hbrbc_stage_name": (ctypes.c_char_p, [ctypes.c_int]),
         "hbrbc_encode_kernel": (ctypes.c_char_p, [_P]),
+        "hbrbc_wire_proof_message_len": (_S, [_S, _S]),
+        "hbrbc_wire_encode_batch": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _S, _S, _S, _S, _P, _P,
+                                                   _P, _P, _S, _S, _P, _S, _P, _P]),
+        "hbrbc_wire_decode_batch": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _P, _P, _P, _P,
+                                                   _P, _P, _P]),
         "hbrbc_jit_build_encode": (ctypes.c_int, [_S, _S, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
@@ -443,6 +450,35 @@ class RbcBatch:
                                         nodes.stride(0), _ptr(payload_out),
                                         payload_out.stride(0), _ptr(plen_out), _ptr(status),
                                         self._stream(stream)))
+
+    # -- bincode wire format of broadcast::Message (message.rs:13-24) -------------
+    def wire_slot(self, S):
+        """Message slot bytes for Value/Echo messages of S-byte shards."""
+        return (lib().hbrbc_wire_proof_message_len(S, self.dslots) + 15) // 16 * 16
+
+    def wire_encode(self, values, S, digests, ndig, roots, out, msg_len, variant=0, indices=None,
+                    stream=None):
+        """Value (variant 0) or Echo (1) messages of proofs laid out as for
+        validate_rows: values [count, per_inst, >=S] (16-aligned rows), digests
+        [count, per_inst, dslots, 32], ndig [count, per_inst], roots [count, >=32];
+        out uint8 [count*per_inst, slot], msg_len int32 [count*per_inst]."""
+        count, per_inst = values.shape[0], values.shape[1]
+        _check(lib().hbrbc_wire_encode_batch(self.coding.handle, variant, _ptr(values), S,
+                                             values.stride(1), values.stride(0), per_inst,
+                                             _ptr(indices), _ptr(digests), _ptr(ndig),
+                                             _ptr(roots), roots.stride(0), count, _ptr(out),
+                                             out.stride(0), _ptr(msg_len), self._stream(stream)))
+
+    def wire_decode(self, msgs, msg_len, values, value_len, index, digests, ndig, roots, variant,
+                    status, stream=None):
+        """Parse msgs uint8 [nmsg, slot] (msg_len int32 [nmsg]) into values
+        [nmsg, stride], value_len/index/variant/status int32 [nmsg], digests
+        [nmsg, dslots, 32], ndig uint8 [nmsg], roots [nmsg, 32]."""
+        _check(lib().hbrbc_wire_decode_batch(self.coding.handle, _ptr(msgs), msgs.stride(0),
+                                             _ptr(msg_len), msgs.shape[0], _ptr(values),
+                                             values.stride(0), _ptr(value_len), _ptr(index),
+                                             _ptr(digests), _ptr(ndig), _ptr(roots), _ptr(variant),
+                                             _ptr(status), self._stream(stream)))
 
     def reserve(self, count):
         _check(lib().hbrbc_reserve(self.coding.handle, count))

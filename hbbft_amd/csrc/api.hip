@@ -978,6 +978,85 @@ int hbrbc_proof_validate(const uint8_t *value, size_t len, size_t index, const u
     return HBRBC_OK;
 }
 
+// ------------------------------------------------------------ wire format --
+size_t hbrbc_wire_proof_message_len(size_t value_len, size_t ndig) { return 60 + value_len + 32 * ndig; }
+
+int hbrbc_wire_encode_batch(hbrbc_ctx *c, uint32_t variant, const uint8_t *values, size_t value_len,
+                            size_t value_stride, size_t value_inst_stride, size_t per_inst,
+                            const uint32_t *indices, const uint8_t *digests, const uint8_t *ndig,
+                            const uint8_t *roots, size_t root_stride, size_t count, uint8_t *out,
+                            size_t msg_stride, uint32_t *msg_len_out, void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (count == 0 || per_inst == 0) return HBRBC_OK;
+    if (variant > 1) return fail(HBRBC_E_INVALID_ARG, "variant must be 0 (Value) or 1 (Echo)");
+    const size_t dslots = hbrbc_merkle_max_proof_len(c->n);
+    if (!values || reinterpret_cast<uintptr_t>(values) % 16 || value_stride % 16 ||
+        value_inst_stride % 16 || value_stride < value_len)
+        return fail(HBRBC_E_INVALID_ARG, "values must be 16-byte aligned rows of >= value_len");
+    if (!ndig || !roots || !out || !msg_len_out || (dslots && !digests))
+        return fail(HBRBC_E_INVALID_ARG, "null argument");
+    if (reinterpret_cast<uintptr_t>(out) % 16 || msg_stride % 16 ||
+        msg_stride < round_up(hbrbc_wire_proof_message_len(value_len, dslots), 16))
+        return fail(HBRBC_E_INVALID_ARG, "msg_stride must be a multiple of 16 and >= %zu",
+                    round_up(hbrbc_wire_proof_message_len(value_len, dslots), 16));
+    if (value_len > 0xFFFFFFFFull - 4096) return fail(HBRBC_E_INVALID_ARG, "value too long");
+    HB_HIP(hipSetDevice(c->device));
+    WireEncodeArgs a;
+    a.variant = variant;
+    a.values = values;
+    a.value_len = value_len;
+    a.value_stride = value_stride;
+    a.value_inst_stride = value_inst_stride;
+    a.per_inst = per_inst;
+    a.indices = indices;
+    a.digests = digests;
+    a.dslots = dslots;
+    a.ndig = ndig;
+    a.roots = roots;
+    a.root_stride = root_stride;
+    a.count = count;
+    a.out = out;
+    a.msg_stride = msg_stride;
+    a.msg_len = msg_len_out;
+    HB_HIP(launch_wire_encode(a, pick(c, stream)));
+    return HBRBC_OK;
+}
+
+int hbrbc_wire_decode_batch(hbrbc_ctx *c, const uint8_t *msgs, size_t msg_stride,
+                            const uint32_t *msg_len, size_t nmsg, uint8_t *values,
+                            size_t value_stride, uint32_t *value_len_out, uint32_t *index_out,
+                            uint8_t *digests, uint8_t *ndig_out, uint8_t *roots,
+                            uint32_t *variant_out, int32_t *status_out, void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (nmsg == 0) return HBRBC_OK;
+    const size_t dslots = hbrbc_merkle_max_proof_len(c->n);
+    if (!msgs || reinterpret_cast<uintptr_t>(msgs) % 16 || msg_stride % 16 || !msg_len)
+        return fail(HBRBC_E_INVALID_ARG, "messages must be 16-byte aligned slots");
+    if (!values || reinterpret_cast<uintptr_t>(values) % 16 || value_stride % 16 ||
+        !value_len_out || !index_out || !ndig_out || !roots || !variant_out || !status_out ||
+        (dslots && !digests))
+        return fail(HBRBC_E_INVALID_ARG, "null or misaligned output");
+    HB_HIP(hipSetDevice(c->device));
+    WireDecodeArgs a;
+    a.msgs = msgs;
+    a.msg_stride = msg_stride;
+    a.msg_len = msg_len;
+    a.nmsg = nmsg;
+    a.values = values;
+    a.value_stride = value_stride;
+    a.value_cap = value_stride;
+    a.value_len = value_len_out;
+    a.index = index_out;
+    a.digests = digests;
+    a.dslots = dslots;
+    a.ndig = ndig_out;
+    a.roots = roots;
+    a.variant = variant_out;
+    a.status = status_out;
+    HB_HIP(launch_wire_decode(a, pick(c, stream)));
+    return HBRBC_OK;
+}
+
 // ------------------------------------------------------ specialised encode --
 const char *hbrbc_encode_kernel(const hbrbc_ctx *c) { return c ? c->enc_kind.c_str() : "none"; }
 

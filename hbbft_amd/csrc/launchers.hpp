@@ -91,6 +91,38 @@ hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, size_t shard_
                           const uint32_t *plen, const int32_t *status, uint8_t *payload_out,
                           size_t payload_stride, hipStream_t s);
 
+// bincode wire format of broadcast::Message (wire.hip).
+struct WireEncodeArgs {
+    uint32_t variant;           // 0 Value, 1 Echo
+    const uint8_t *values;
+    size_t value_len, value_stride, value_inst_stride, per_inst;
+    const uint32_t *indices;    // [count][per_inst] or nullptr (index = j)
+    const uint8_t *digests;     // [count][per_inst][dslots][32]
+    size_t dslots;
+    const uint8_t *ndig;        // [count][per_inst]
+    const uint8_t *roots;
+    size_t root_stride, count;
+    uint8_t *out;               // [count * per_inst][msg_stride]
+    size_t msg_stride;
+    uint32_t *msg_len;          // [count * per_inst]
+};
+hipError_t launch_wire_encode(const WireEncodeArgs &a, hipStream_t s);
+struct WireDecodeArgs {
+    const uint8_t *msgs;
+    size_t msg_stride;
+    const uint32_t *msg_len;
+    size_t nmsg;
+    uint8_t *values;            // [nmsg][value_stride]
+    size_t value_stride, value_cap;  // value_cap <= value_stride (multiple of 16)
+    uint32_t *value_len, *index;
+    uint8_t *digests;           // [nmsg][dslots][32]
+    size_t dslots;
+    uint8_t *ndig, *roots;      // [nmsg], [nmsg][32]
+    uint32_t *variant;
+    int32_t *status;
+};
+hipError_t launch_wire_decode(const WireDecodeArgs &a, hipStream_t s);
+
 hipError_t configure_kernels();
 
 }  // namespace hbrbc

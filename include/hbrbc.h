@@ -68,6 +68,10 @@ enum hbrbc_status {
     HBRBC_E_SINGULAR_MATRIX = 64,
     HBRBC_E_ROOT_MISMATCH = 65,   /* mtree.root_hash() != root_hash (583-585) */
     HBRBC_E_NO_PAYLOAD_LEN = 66,  /* fewer than 4 data bytes (592-597)        */
+    /* bincode deserialisation of a wire message (hbrbc_wire_decode_batch) */
+    HBRBC_E_WIRE_TRUNCATED = 70,    /* bincode ErrorKind::Io(UnexpectedEof)     */
+    HBRBC_E_WIRE_BAD_VARIANT = 71,  /* enum variant index > 4                   */
+    HBRBC_E_WIRE_TOO_LARGE = 72,    /* value or digest list exceeds the batch's slots */
     /* library errors */
     HBRBC_E_INVALID_ARG = 100,
     HBRBC_E_DEVICE = 101,         /* a HIP call failed: see hbrbc_last_error() */
@@ -188,6 +192,40 @@ int hbrbc_decode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t
                        uint32_t *payload_len_out, int32_t *status_out, void *stream);
 /* Pre-size the reconstruct workspace for `count` instances. */
 int hbrbc_reserve(hbrbc_ctx *ctx, size_t count);
+
+/* ---- wire format: bincode of broadcast::Message -------------------------- */
+/* `Message::{Value, Echo}(Proof<Vec<u8>>)` (message.rs:13-24, merkle.rs:72-78) as
+ * bincode 1.x `serialize` writes it (Cargo.toml:24; examples/simulation.rs:132,
+ * examples/network/commst.rs:68): u32 LE variant (0 Value, 1 Echo, 2 Ready,
+ * 3 CanDecode, 4 EchoHash), then for Value/Echo u64 LE value length, the value,
+ * u64 LE index, u64 LE digest count, 32 bytes per digest, 32 root bytes;
+ * for the digest variants 32 bytes.  Message g lives in a slot at
+ * out + g*msg_stride (16-aligned, zero-padded past its length). */
+size_t hbrbc_wire_proof_message_len(size_t value_len, size_t ndig);
+/* Serialise the proofs laid out as for hbrbc_validate_batch (value (i, j) at
+ * values + i*value_inst_stride + j*value_stride, 16-aligned rows; index
+ * indices[i*per_inst + j] or j; digests/ndig as hbrbc_proofs_batch; root at
+ * roots + i*root_stride) as Value (variant 0) or Echo (1) messages, message
+ * g = i*per_inst + j; msg_len_out[g] = its length.  msg_stride >=
+ * round_up(proof_message_len(value_len, max_proof_len(n)), 16). */
+int hbrbc_wire_encode_batch(hbrbc_ctx *ctx, uint32_t variant, const uint8_t *values,
+                            size_t value_len, size_t value_stride, size_t value_inst_stride,
+                            size_t per_inst, const uint32_t *indices, const uint8_t *digests,
+                            const uint8_t *ndig, const uint8_t *roots, size_t root_stride,
+                            size_t count, uint8_t *out, size_t msg_stride, uint32_t *msg_len_out,
+                            void *stream);
+/* Deserialise `nmsg` messages of msg_len[g] bytes each (bincode `deserialize`;
+ * trailing bytes ignored): variant_out[g]; for Value/Echo the value into
+ * values + g*value_stride (zero-padded; longer than value_stride -> WIRE_TOO_LARGE),
+ * value_len_out, index_out (saturated at 2^32-1), digests + g*max_proof_len(n)*32
+ * and ndig_out (more than max_proof_len(n) -> WIRE_TOO_LARGE, since no tree over
+ * n leaves has that many levels), roots + g*32; for Ready/CanDecode/EchoHash the
+ * digest into roots.  status_out[g] = OK or a WIRE_* code. */
+int hbrbc_wire_decode_batch(hbrbc_ctx *ctx, const uint8_t *msgs, size_t msg_stride,
+                            const uint32_t *msg_len, size_t nmsg, uint8_t *values,
+                            size_t value_stride, uint32_t *value_len_out, uint32_t *index_out,
+                            uint8_t *digests, uint8_t *ndig_out, uint8_t *roots,
+                            uint32_t *variant_out, int32_t *status_out, void *stream);
 
 /* ---- specialised encoder ------------------------------------------------ */
 /* Coding::encode runs either the generic bit-sliced GF kernel or, when a code

@@ -222,3 +222,51 @@ def bench_pipeline(n, f, plen, count, n_erase, seed, threads):
     ok = c_size_t(0)
     t = lib().orc_bench_pipeline(n, f, plen, count, n_erase, seed, threads, ctypes.byref(ok))
     return t, ok.value
+
+
+# ---- bincode wire format of broadcast::Message ------------------------------
+# bincode 1.x defaults (Cargo.toml:24 `bincode = "1.2.0"`; serialize at
+# examples/simulation.rs:132): little-endian fixed-width integers, enum
+# variant as u32, Vec length and usize as u64, [u8; 32] as 32 raw bytes.
+# Field order of Proof: value, index, digests, root_hash (merkle.rs:72-78);
+# variants in declaration order (message.rs:13-24).  Plain struct packing:
+# restated from the bincode 1.x specification, no reference fixture exists.
+import struct as _struct
+
+WIRE_VARIANTS = {"Value": 0, "Echo": 1, "Ready": 2, "CanDecode": 3, "EchoHash": 4}
+
+
+def bincode_message(variant, value=b"", index=0, digests=(), root=b"\0" * 32):
+    v = WIRE_VARIANTS[variant] if isinstance(variant, str) else variant
+    if v >= 2:
+        return _struct.pack("<I", v) + bytes(root)
+    digests = [bytes(d) for d in digests]
+    return (_struct.pack("<IQ", v, len(value)) + bytes(value) + _struct.pack("<QQ", index, len(digests))
+            + b"".join(digests) + bytes(root))
+
+
+def bincode_parse(msg):
+    """-> (variant, value, index, digests, root) or raises ValueError (truncated /
+    bad variant), as bincode::deserialize::<Message> would fail."""
+    msg = bytes(msg)
+    if len(msg) < 4:
+        raise ValueError("truncated")
+    (v,) = _struct.unpack_from("<I", msg, 0)
+    if v > 4:
+        raise ValueError("bad variant")
+    if v >= 2:
+        if len(msg) < 36:
+            raise ValueError("truncated")
+        return v, b"", 0, [], msg[4:36]
+    if len(msg) < 12:
+        raise ValueError("truncated")
+    (L,) = _struct.unpack_from("<Q", msg, 4)
+    if len(msg) < 28 + L:
+        raise ValueError("truncated")
+    value = msg[12:12 + L]
+    index, d = _struct.unpack_from("<QQ", msg, 12 + L)
+    if len(msg) < 60 + L + 32 * d:
+        raise ValueError("truncated")
+    digests = [msg[28 + L + 32 * t: 60 + L + 32 * t] for t in range(d)]
+    root = msg[28 + L + 32 * d: 60 + L + 32 * d]
+    return v, value, index, digests, root

@@ -156,3 +156,23 @@ def test_unframe_truncates_and_rejects_short():
 def test_bench_pipeline_small():
     t, ok = orc.bench_pipeline(16, 5, 4096, 8, 5, 1, 2)
     assert ok == 8 and t > 0
+
+
+def test_bincode_wire_vectors():
+    """Wire format of broadcast::Message (bincode 1.x), golden N=4 'Foo' messages."""
+    w = load("wire_vectors.json")
+    sh, nd = orc.send_shards(4, 1, b"Foo")
+    root = nd[-1].tobytes()
+    assert root.hex() == w["root"]
+    for j_s, hx in w["value_msgs"].items():
+        j = int(j_s)
+        p = orc.merkle_proof(nd, 4, j)
+        msg = orc.bincode_message("Value", sh[j].tobytes(), j, [d.tobytes() for d in p], root)
+        assert msg.hex() == hx
+        v, value, index, digests, r = orc.bincode_parse(msg)
+        assert (v, value, index, r) == (0, sh[j].tobytes(), j, root)
+        assert digests == [d.tobytes() for d in p]
+    assert orc.bincode_message("Ready", root=root).hex() == w["ready"]
+    for bad in [b"\x00\x00\x00", b"\x05\x00\x00\x00" + bytes(32), bytes.fromhex(w["value_msgs"]["0"])[:-1]]:
+        with pytest.raises(ValueError):
+            orc.bincode_parse(bad)
