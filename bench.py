@@ -24,6 +24,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_OPS = 78.6e12        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (32-bit lane-ops/s)
 KECCAK_OPS_PER_PERM = 4320     # ~180 VALU ops/round x 24 rounds
+# measured ceiling of the Keccak-f[1600] round code itself (register-only loop,
+# 4 waves/SIMD, profiles/r1_valu_microbench.txt): v_alignbit issues at half rate
+KECCAK_CEILING_PERMS = 10.48e9
 
 CONFIGS = {
     # name: (N, payload bytes, instances per GPU, erasures)
@@ -124,8 +127,7 @@ def main():
         subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
 
     def run_sub(sb, sl):
-        sb.frame(payloads[sl], plen, slab[sl])
-        sb.encode(slab[sl], S)
+        sb.frame_encode(payloads[sl], plen, slab[sl])   # frame folded into the encoder
         sb.merkle(slab[sl], S, nodes[sl])
         sb.proofs(nodes[sl], digests[sl], ndig[sl])
         sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
@@ -207,8 +209,11 @@ def main():
     valu = None
     if dom in perms:
         ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
+        pps = perms[dom] / per_launch_s
         valu = {"achieved_ops": ops, "peak_ops": VALU_PEAK_OPS, "frac": ops / VALU_PEAK_OPS,
-                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom]}
+                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom],
+                "perms_per_s": pps, "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
+                "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS}
     step_bytes = sum(alg_bytes[s] * (stages[s][1] / max(args.steps, 1)) for s in stages)
     roofline = {
         "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -344,8 +349,11 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
     valu = None
     if dom in perms:
         ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
+        pps = perms[dom] / per_launch_s
         valu = {"achieved_ops": ops, "peak_ops": VALU_PEAK_OPS, "frac": ops / VALU_PEAK_OPS,
-                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom]}
+                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom],
+                "perms_per_s": pps, "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
+                "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS}
     xbytes = 2 * (world - 1) / world * count * sb.topo.npad * sb.stride
     value = float(count) * plen * world * args.steps / elapsed / 1e9
     if rank == 0:

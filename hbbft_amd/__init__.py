@@ -82,6 +82,7 @@ def lib():
         "hbrbc_shard_len": (_S, [_S, _S]),
         "hbrbc_frame_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _S, _S, _P]),
         "hbrbc_encode_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P]),
+        "hbrbc_frame_encode_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _S, _S, _P]),
         "hbrbc_merkle_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P, _S, _P]),
         "hbrbc_proofs_batch": (ctypes.c_int, [_P, _P, _S, _S, _P, _P, _P]),
         "hbrbc_validate_batch": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P, _P, _P, _P, _S, _S,
@@ -396,6 +397,14 @@ class RbcBatch:
         _check(lib().hbrbc_frame_batch(self.coding.handle, _ptr(payloads), payloads.stride(0),
                                        plen, count, _ptr(slab), S, slab.stride(1),
                                        slab.stride(0), self._stream(stream)))
+
+    def frame_encode(self, payloads, plen, slab, stream=None):
+        """frame + encode in one pass when the specialised encoder is loaded."""
+        count = slab.shape[0]
+        S = shard_len(plen, self.k)
+        _check(lib().hbrbc_frame_encode_batch(self.coding.handle, _ptr(payloads), payloads.stride(0),
+                                              plen, count, _ptr(slab), S, slab.stride(1),
+                                              slab.stride(0), self._stream(stream)))
 
     def encode(self, slab, S, stream=None):
         _check(lib().hbrbc_encode_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),

@@ -167,6 +167,7 @@ struct hbrbc_ctx {
     // specialised encoder (jit.hip) for this matrix, when its code object is available
     hipModule_t enc_mod = nullptr;
     hipFunction_t enc_fn = nullptr;
+    hipFunction_t fe_fn = nullptr;   // its frame+encode twin
     int rt_spec = 2;              // parity rows per pass of the specialised encoder
     int depth_spec = 4;           // its data-row prefetch depth
     std::string enc_kind = "none";
@@ -349,7 +350,7 @@ std::string jit_dir() {
 }
 
 std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth) {
-    return dir + "/" + encode_kernel_name(k, m, rt, depth) + "_v3.co";
+    return dir + "/" + encode_kernel_name(k, m, rt, depth, false) + "_v5.co";
 }
 
 // Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).
@@ -406,11 +407,16 @@ void setup_spec_encoder(hbrbc_ctx *c) {
         return;
     }
     if (hipModuleGetFunction(&c->enc_fn, c->enc_mod,
-                             encode_kernel_name(c->k, c->m, c->rt_spec, c->depth_spec).c_str()) !=
-        hipSuccess) {
+                             encode_kernel_name(c->k, c->m, c->rt_spec, c->depth_spec, false)
+                                 .c_str()) != hipSuccess ||
+        hipModuleGetFunction(&c->fe_fn, c->enc_mod,
+                             encode_kernel_name(c->k, c->m, c->rt_spec, fused_depth(c->depth_spec),
+                                                true)
+                                 .c_str()) != hipSuccess) {
         (void)hipModuleUnload(c->enc_mod);
         c->enc_mod = nullptr;
         c->enc_fn = nullptr;
+        c->fe_fn = nullptr;
         return;
     }
     c->enc_kind = "specialised";
@@ -642,6 +648,49 @@ int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     g.nin = (int)c->k;
     g.count = count;
     HB_HIP(launch_gf_apply(g, s));
+    return HBRBC_OK;
+}
+
+int hbrbc_frame_encode_batch(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stride,
+                             size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
+                             size_t shard_stride, size_t inst_stride, void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (count == 0) return HBRBC_OK;
+    const bool fused = c->fe_fn && shard_stride == round_up(shard_len, 16) &&
+                       shard_len == hbrbc_shard_len(payload_len, c->k) &&
+                       payload_len <= 0x7FFFFFFFull && shard_len * c->k < 0x7FFFFFFFull;
+    if (!fused) {
+        int st = hbrbc_frame_batch(c, payloads, payload_stride, payload_len, count, shards,
+                                   shard_len, shard_stride, inst_stride, stream);
+        return st ? st : hbrbc_encode_batch(c, shards, shard_len, shard_stride, inst_stride, count,
+                                            stream);
+    }
+    if (payload_len && (!payloads || reinterpret_cast<uintptr_t>(payloads) % 4 ||
+                        payload_stride % 4 || payload_stride < round_up(payload_len, 4)))
+        return fail(HBRBC_E_INVALID_ARG, "payload buffer must be 4-byte aligned with stride >= "
+                                         "round_up(len, 4)");
+    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
+    if (st) return st;
+    HB_HIP(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    StageTimer t(c, HBRBC_STAGE_ENCODE, s);
+    // frame folded into the specialised encoder (jit.hip): the data rows are
+    // written by pass 0 from the payloads, parity from the same registers
+    uint8_t *base = shards;
+    const uint8_t *pay = payloads;
+    unsigned long ist = inst_stride, sst = shard_stride, pst = payload_stride;
+    unsigned row_bytes = (unsigned)shard_stride, P = (unsigned)payload_len, S = (unsigned)shard_len;
+    unsigned wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
+    const size_t blocks = (size_t)wpr * count;
+    if (blocks > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "grid too large");
+    const int npass = (int)((c->m + c->rt_spec - 1) / c->rt_spec);
+    const unsigned threads = 64u * (unsigned)std::min(4, npass);
+    void *args[] = {&base, &ist, &sst, &row_bytes, &wpr, &pay, &pst, &P, &S};
+    HB_HIP(hipModuleLaunchKernel(c->fe_fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args,
+                                 nullptr));
+    HB_HIP(launch_frame_fixup(payloads, payload_stride, payload_len, shards, shard_len,
+                              shard_stride, inst_stride, c->k, c->m, c->d_matrix.as<uint8_t>(),
+                              count, s));
     return HBRBC_OK;
 }
 

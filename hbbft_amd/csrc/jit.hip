@@ -19,7 +19,7 @@
 // rows.  Output is bit-identical to the generic kernels (tests compare both
 // with the oracle).
 //
-// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_v3.co);
+// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_v5.co);
 // __graft_entry__.build() pre-generates them for the BASELINE validator
 // counts, and a context loads the file when present.  Compiling a missing
 // one at context creation is opt-in (HBRBC_JIT=1) since it takes seconds.
@@ -55,6 +55,27 @@ const char *kPrelude = R"(
 typedef unsigned int uint32_t;
 typedef unsigned char uint8_t;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 32 bytes starting `bs` (0..3, wave-uniform) bytes into the 36 loaded bytes
+// (q0, q1, q2[0]): eight v_alignbyte with a scalar shift
+__device__ __forceinline__ void hb_window(const u32x4 q0, const u32x4 q1, const uint32_t q2,
+                                          unsigned bs, uint32_t (&o)[8]) {
+    const uint32_t w[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2};
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs);
+}
+// Framed bytes [lb, lb + 32) built byte by byte: the rare windows that touch
+// the 4-byte BE32 length prefix (only lanes at offset 0 of rows starting
+// before logical byte 4).  pay = the instance's payload row.
+__device__ __forceinline__ void hb_frame_slow(const uint8_t *pay, unsigned P, unsigned lb,
+                                              uint32_t (&x)[8]) {
+    for (int i = 0; i < 8; ++i) x[i] = 0u;
+    for (unsigned i = 0; i < 32u; ++i) {
+        const unsigned b = lb + i;
+        // payload bytes past P & ~3 are left 0 here as in the fast path: the
+        // host's frame_fixup kernel adds them (and their parity) afterwards
+        const unsigned v = b < 4u ? (P >> (8u * (3u - b))) & 0xFFu : (b - 4u < (P & ~3u) ? pay[b - 4u] : 0u);
+        x[i >> 2] |= v << (8u * (i & 3u));
+    }
+}
 // 8x32 bit transpose of 8 dwords (three delta swaps; an involution)
 __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
 #pragma unroll
@@ -75,20 +96,25 @@ __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
 
 }  // namespace
 
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth) {
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, bool fused) {
     char b[96];
-    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d", k, m, rt, depth);
+    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d%s", k, m, rt, depth, fused ? "_fe" : "");
     return b;
 }
 
-std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth) {
+std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
+                              bool fused) {
     const int npass = (int)((m + rt - 1) / rt);
+    if (fused) depth = fused_depth(depth);  // 36 bytes per row in flight
     const int nbuf = depth + 1;
     std::ostringstream o;
-    o << kPrelude;
-    o << "extern \"C\" __global__ __launch_bounds__(256) void " << encode_kernel_name(k, m, rt, depth)
+    o << "\nextern \"C\" __global__ __launch_bounds__(256) void "
+      << encode_kernel_name(k, m, rt, depth, fused)
       << "(uint8_t *__restrict__ base, unsigned long inst_stride, unsigned long shard_stride,\n"
-         "    unsigned row_bytes, unsigned waves_per_row) {\n"
+         "    unsigned row_bytes, unsigned waves_per_row"
+      << (fused ? ", const uint8_t *__restrict__ payloads, unsigned long payload_stride,\n"
+                  "    unsigned P, unsigned S" : "")
+      << ") {\n"
          "  const unsigned long inst = blockIdx.x / waves_per_row;\n"
          "  const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);\n"
          "  const unsigned chunk = (blockIdx.x - (unsigned)inst * waves_per_row) * 64u + (threadIdx.x & 63u);\n"
@@ -104,32 +130,85 @@ std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, in
          "      base + inst * inst_stride, (short)0, 0x7fffffff, 0x00020000);\n"
          "  const unsigned sst = (unsigned)shard_stride;\n"
          "#define HB_LD(L, H, j) { L = __builtin_amdgcn_raw_buffer_load_b128(rs, off, (j) * sst, 0); "
-         "H = __builtin_amdgcn_raw_buffer_load_b128(rs, off2, (j) * sst, 0); }\n"
-         "  for (int p = __builtin_amdgcn_readfirstlane(wave); p < "
-      << npass << "; p += nw) {\n    switch (p) {\n";
+         "H = __builtin_amdgcn_raw_buffer_load_b128(rs, off2, (j) * sst, 0); }\n";
+    if (fused)
+        // framing (broadcast.rs:174-189) folded into the loads: logical byte b
+        // of the framed value is payload byte b - 4.  The buffer resource
+        // covers the whole dwords of the payload (P & ~3 bytes; range checks
+        // are per dword), so everything past them reads 0; the 0-3 bytes of a
+        // partial last dword are added, with their parity, by frame_fixup.
+        o << "  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "      (void *)(payloads + inst * payload_stride), (short)0, (int)(P & ~3u), 0x00020000);\n"
+             "  const bool edge = !__all(off + 32u <= S);\n"
+             // dword-aligned start: the 32 framed bytes of a lane are bytes
+             // bs..bs+31 of 36 loaded bytes, bs = (j*S - 4) & 3 (uniform per row)
+             // (the address add is volatile asm: LLVM would otherwise hoist every
+             // row's address out of the pass loop and keep k of them live)
+             "#define HB_LDF(Q0, Q1, Q2, j) { unsigned a_; "
+             "__asm__ volatile(\"v_add_u32 %0, %1, %2\" : \"=v\"(a_) : \"s\"((j) * S - 4u), \"v\"(off)); "
+             "a_ &= ~3u; "
+             "Q0 = __builtin_amdgcn_raw_buffer_load_b128(pr, a_, 0, 0); "
+             "Q1 = __builtin_amdgcn_raw_buffer_load_b128(pr, a_ + 16u, 0, 0); "
+             "Q2 = __builtin_amdgcn_raw_buffer_load_b32(pr, a_ + 32u, 0, 0); }\n";
+    o << "  for (int p = __builtin_amdgcn_readfirstlane(wave); p < " << npass
+      << "; p += nw) {\n    switch (p) {\n";
     for (int p = 0; p < npass; ++p) {
         const int r0 = p * rt;
         const int rows = (int)std::min<size_t>((size_t)rt, m - (size_t)r0);
         // a distinct barrier opens every case, so no common prefix (the first
         // rows' loads) is hoisted above the switch and kept live across it
         o << "    case " << p << ": {\n      __asm__ volatile(\"; pass " << p
-          << "\" ::: \"memory\");\n      uint32_t a[" << rows << "][8] = {};\n"
-          << "      u32x4 l[" << nbuf << "], h[" << nbuf << "];\n";
-        // rows 0..depth-1 in flight before the first product; row j + depth is
-        // requested while row j is consumed (depth rows of HBM latency hidden)
-        for (int j = 0; j < depth && j < (int)k; ++j)
-            o << "      HB_LD(l[" << j << "], h[" << j << "], " << j << ") __asm__ volatile(\"\" ::: \"memory\");\n";
-        for (size_t j = 0; j < k; ++j) {
-            const int cur = (int)(j % nbuf);
+          << "\" ::: \"memory\");\n      uint32_t a[" << rows << "][8] = {};\n";
+        if (fused)
+            o << "      u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "];\n";
+        else
+            o << "      u32x4 l[" << nbuf << "], h[" << nbuf << "];\n";
+        auto load = [&](size_t j) {
+            const int b = (int)(j % nbuf);
+            if (fused)
+                o << "      HB_LDF(q0[" << b << "], q1[" << b << "], q2[" << b << "], " << j << "u)";
+            else
+                o << "      HB_LD(l[" << b << "], h[" << b << "], " << j << ")";
             // the empty asm keeps the scheduler from hoisting every row's load to
             // the top of the straight-line pass (hundreds of live VGPRs)
-            if (j + depth < k)
-                o << "      HB_LD(l[" << (j + depth) % nbuf << "], h[" << (j + depth) % nbuf << "], "
-                  << j + depth << ") __asm__ volatile(\"\" ::: \"memory\");\n";
-            const std::string lc = "l[" + std::to_string(cur) + "]";
-            o << "      { const u32x4 hh = full ? h[" << cur << "] : (u32x4)(0u);\n"
-              << "        uint32_t x[8] = {" << lc << "[0], " << lc << "[1], " << lc << "[2], " << lc
-              << "[3], hh[0], hh[1], hh[2], hh[3]};\n        hb_tr(x);\n";
+            o << " __asm__ volatile(\"\" ::: \"memory\");\n";
+        };
+        // rows 0..depth-1 in flight before the first product; row j + depth is
+        // requested while row j is consumed (depth rows of HBM latency hidden)
+        for (int j = 0; j < depth && j < (int)k; ++j) load((size_t)j);
+        for (size_t j = 0; j < k; ++j) {
+            const int cur = (int)(j % nbuf);
+            if (j + depth < k) load(j + depth);
+            if (fused) {
+                const std::string c = std::to_string(cur);
+                o << "      { uint32_t x[8];\n"
+                  << "        hb_window(q0[" << c << "], q1[" << c << "], q2[" << c << "], (" << j
+                  << "u * S - 4u) & 3u, x);\n";
+                // windows touching the BE32 payload length (broadcast.rs:175-177);
+                // j * S < 4 needs j < 4 since S >= 1
+                if (j < 4)
+                    o << "        if (" << j << "u * S < 4u) { if (off == 0u) hb_frame_slow(payloads + inst * "
+                     "payload_stride, P, " << j << "u * S, x); }\n";
+                // positions >= S of this row belong to the next shard: zero
+                o << "        if (edge) {\n"
+                     "          _Pragma(\"unroll\") for (int i_ = 0; i_ < 8; ++i_) {\n"
+                     "            const int lim_ = (int)S - (int)off - 4 * i_;\n"
+                     "            x[i_] = lim_ >= 4 ? x[i_] : (lim_ <= 0 ? 0u : x[i_] & (0xFFFFFFFFu >> (8 * (4 - lim_))));\n"
+                     "          }\n        }\n";
+                if (p == 0)  // pass 0 also writes the framed data row
+                    o << "        if (active) {\n"
+                         "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[0], x[1], x[2], x[3]}, rs, off, "
+                      << j << "u * sst, 0);\n"
+                         "          if (full) __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[4], x[5], x[6], x[7]}, "
+                         "rs, off2, "
+                      << j << "u * sst, 0);\n        }\n";
+                o << "        hb_tr(x);\n";
+            } else {
+                const std::string lc = "l[" + std::to_string(cur) + "]";
+                o << "      { const u32x4 hh = full ? h[" << cur << "] : (u32x4)(0u);\n"
+                  << "        uint32_t x[8] = {" << lc << "[0], " << lc << "[1], " << lc << "[2], " << lc
+                  << "[3], hh[0], hh[1], hh[2], hh[3]};\n        hb_tr(x);\n";
+            }
             // Term lists of every (row, plane): output plane q of c*x is the
             // XOR of the planes p with bit q of c*2^p set.  Terms are paired in
             // order ((p1,p2), (p3,p4), ...); the pair XORs are computed once per
@@ -191,6 +270,11 @@ std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, in
     }
     o << "    }\n  }\n}\n";
     return o.str();
+}
+
+std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth) {
+    return std::string(kPrelude) + gen_encode_kernel(k, m, parity_rows, rt, depth, false) +
+           gen_encode_kernel(k, m, parity_rows, rt, depth, true);
 }
 
 int compile_encode(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,

@@ -134,6 +134,31 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(
     *dst = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// ----------------------------------------------------------- frame fixup --
+// The fused frame+encode kernel (jit.hip) reads the payload in whole dwords;
+// the last P & 3 payload bytes are added here: each is written into its data
+// row and, GF(2^8) being linear, c * byte is XORed into every parity row at
+// the same position (c = M[k + r][row]).  One thread per instance.
+__global__ __launch_bounds__(kBlock) void frame_fixup_kernel(
+    const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P,
+    uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
+    uint32_t k, uint32_t m, const uint8_t *__restrict__ matrix, size_t count) {
+    const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
+    if (inst >= count) return;
+    const uint8_t *pay = payloads + inst * payload_stride;
+    uint8_t *ib = shards + inst * inst_stride;
+    for (uint32_t t = P & ~3u; t < P; ++t) {
+        const uint8_t v = pay[t];
+        const uint32_t b = t + 4, j = b / S, pos = b - j * S;
+        ib[(size_t)j * shard_stride + pos] = v;
+        if (!v) continue;
+        for (uint32_t r = 0; r < m; ++r) {
+            const uint8_t c = matrix[(size_t)(k + r) * k + j];
+            if (c) ib[(size_t)(k + r) * shard_stride + pos] ^= kGf.exp[kGf.log[c] + kGf.log[v]];
+        }
+    }
+}
+
 // -------------------------------------------------------------- GF apply --
 // Split-2-bit v_perm_b32 GF(2^8) multiply-accumulate over 16-byte chunks.
 // Every lane owns 16 consecutive byte positions of all rows.  Output rows
@@ -747,6 +772,18 @@ hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t p
     hipLaunchKernelGGL(frame_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, payloads,
                        payload_stride, (uint32_t)payload_len, shards, (uint32_t)shard_len,
                        shard_stride, inst_stride, (uint32_t)data_shards, (uint32_t)bpr);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_fixup(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
+                              uint8_t *shards, size_t shard_len, size_t shard_stride,
+                              size_t inst_stride, size_t k, size_t m, const uint8_t *matrix,
+                              size_t count, hipStream_t s) {
+    if (count == 0 || (payload_len & 3) == 0) return hipSuccess;
+    hipLaunchKernelGGL(frame_fixup_kernel, dim3(grid_for(count, (size_t)1 << 30)), dim3(kBlock), 0,
+                       s, payloads, payload_stride, (uint32_t)payload_len, shards,
+                       (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)k, (uint32_t)m,
+                       matrix, count);
     return hipGetLastError();
 }
 

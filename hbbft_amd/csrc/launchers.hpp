@@ -13,6 +13,13 @@ hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t p
                         size_t count, uint8_t *shards, size_t shard_len, size_t shard_stride,
                         size_t inst_stride, size_t data_shards, hipStream_t s);
 
+// The last payload_len & 3 payload bytes of a fused frame+encode: data byte
+// plus its GF(2^8) contribution to every parity row (matrix = n x k, device).
+hipError_t launch_frame_fixup(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
+                              uint8_t *shards, size_t shard_len, size_t shard_stride,
+                              size_t inst_stride, size_t k, size_t m, const uint8_t *matrix,
+                              size_t count, hipStream_t s);
+
 // out_row[r] = sum_j C[r][j] * in_row[in_idx[j]] on 16-byte chunks, for
 // nout (per instance or uniform) output rows out_idx[r].
 struct GfApplyArgs {

@@ -213,8 +213,7 @@ class ShardedBroadcast:
     def propose(self, payloads):
         rb, S = self.rb, self.S
         slab = self.slab[:, : self.topo.n]
-        rb.frame(payloads, self.plen, slab)
-        rb.encode(slab, S)
+        rb.frame_encode(payloads, self.plen, slab)
         rb.merkle(slab, S, self.nodes)
         rb.proofs(self.nodes, self.digests, self.ndig)
 

@@ -146,6 +146,14 @@ int hbrbc_frame_batch(hbrbc_ctx *ctx, const uint8_t *payloads, size_t payload_st
  * data..n-1 of every instance written in place. */
 int hbrbc_encode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t shard_stride,
                        size_t inst_stride, size_t count, void *stream);
+/* send_shards' framing + Coding::encode in one pass (broadcast.rs:174-193):
+ * with the specialised encoder loaded and shard_stride == round_up(shard_len,
+ * 16) the data rows are framed straight from the payloads inside the encode
+ * kernel (one read of the payload, no re-read of the data rows); otherwise
+ * hbrbc_frame_batch then hbrbc_encode_batch.  Same arguments and result. */
+int hbrbc_frame_encode_batch(hbrbc_ctx *ctx, const uint8_t *payloads, size_t payload_stride,
+                             size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
+                             size_t shard_stride, size_t inst_stride, void *stream);
 /* MerkleTree::from_vec over the n = data+parity shards of every instance
  * (broadcast.rs:204, 580). */
 int hbrbc_merkle_batch(hbrbc_ctx *ctx, const uint8_t *shards, size_t shard_len,

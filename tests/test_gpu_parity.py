@@ -351,3 +351,32 @@ def test_baseline_contexts_use_the_specialised_encoder(torch_cuda):
     by the product path for the BASELINE validator counts."""
     for n in (4, 16, 64, 128):
         assert hb.Coding.for_validators(n).encode_kernel() == "specialised", n
+
+
+@pytest.mark.parametrize("n,plen,count", [(4, 0, 2), (4, 1, 2), (4, 3, 2), (4, 1024, 3), (4, 61, 2),
+                                          (16, 6001, 3), (16, 1 << 16, 2), (16, 7, 2),
+                                          (64, 11916 * 22 - 4, 2), (64, 5000, 3), (64, 87, 2),
+                                          (128, 10000, 2), (128, 200, 2), (7, 100, 2)])
+def test_frame_encode_fused_vs_oracle(torch_cuda, n, plen, count):
+    """hbrbc_frame_encode_batch (framing folded into the specialised encoder
+    for N = 4, 16, 64, 128; frame + encode otherwise) writes exactly the
+    oracle's shards, zero padding included."""
+    torch = torch_cuda
+    f = (n - 1) // 3
+    rb = hb.RbcBatch(n, f, device=0)
+    S = hb.shard_len(plen, rb.k)
+    pay = np.stack([orc.gen_payload(77, i, plen) for i in range(count)]) if plen else \
+        np.zeros((count, 0), np.uint8)
+    pstride = max(16, (plen + 15) // 16 * 16)
+    payloads = torch.full((count, pstride), 0xC3, dtype=torch.uint8, device="cuda")  # junk past P
+    if plen:
+        payloads[:, :plen] = torch.from_numpy(pay).cuda()
+    slab = rb.alloc_slab(count, S)
+    slab.fill_(0x5A)
+    rb.frame_encode(payloads, plen, slab)
+    torch.cuda.synchronize()
+    sl = slab.cpu().numpy()
+    for i in range(count):
+        sh, _ = orc.send_shards(n, f, pay[i].tobytes())
+        assert np.array_equal(sl[i, :, :S], sh), (n, plen, i)
+        assert not sl[i, :, S:].any(), "padding must be zero"
