@@ -191,7 +191,8 @@ def main():
     # algorithmic bytes per launch (SURVEY 8d per-instance figures x instances per launch)
     alg_bytes = {s_: per_launch * v_ for s_, v_ in {
         "frame": plen + k * S,
-        "encode": (k + m) * S,
+        # frame folded into the specialised encoder: the encode launch also reads the payload
+        "encode": (k + m) * S + (plen if stages.get("frame", (0.0, 0))[1] == 0 else 0),
         "leaf_hash": n * (S + 32),
         "tree_levels": (rb.node_count - n) * 96,   # one record = all levels of one tree batch
         "proofs": n * rb.dslots * 32 * 2 + n,
