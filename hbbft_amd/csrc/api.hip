@@ -466,9 +466,17 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
     c->n = data_shards + parity_shards;
     c->rt_enc = gf_row_tile((int)c->m);
     // reconstruct rebuilds f..2f rows per instance in hbbft (f random
-    // erasures typical); tile for the typical count, the worst case costs
-    // one more pass
-    c->rt_rec = gf_row_tile((int)((c->m + 1) / 2));
+    // erasures typical).  A workgroup runs up to 4 waves over the same byte
+    // positions, one pass of rt rows each, so tile the typical count into ~4
+    // passes (measured at N=64: rt 6 -> 3.05 ms, 8 -> 3.3, 12 -> 3.55 per
+    // 16384 instances), but not below 6 rows, where the per-pass transposes
+    // and doublings stop amortising.
+    {
+        const int h = (int)((c->m + 1) / 2);
+        int rt = ((h + 3) / 4 + 1) & ~1;
+        if (rt < 6) rt = (h + 1) & ~1;
+        c->rt_rec = std::max(2, std::min(16, std::max(rt, std::min(6, (h + 1) & ~1))));
+    }
     if (const char *e = getenv("HBRBC_GF")) {
         // bitslice (uniform branches), bitslice_likely (set-bit path inline),
         // bitslice_mask (branch-free masked xor), perm (split-2-bit v_perm)
