@@ -380,3 +380,50 @@ def test_frame_encode_fused_vs_oracle(torch_cuda, n, plen, count):
         sh, _ = orc.send_shards(n, f, pay[i].tobytes())
         assert np.array_equal(sl[i, :, :S], sh), (n, plen, i)
         assert not sl[i, :, S:].any(), "padding must be zero"
+
+
+@pytest.mark.parametrize("n,plen,count,erase", [(16, 1 << 20, 6, "f"), (128, 256 << 10, 8, "f"),
+                                                (250, 4 << 20, 2, "worst")])
+def test_baseline_sizes_roundtrip(torch_cuda, n, plen, count, erase):
+    """The other BASELINE configs at full size (cfg2 N=16 1 MiB, cfg4 N=128
+    256 KiB, cfg5 N=250 4 MiB with only k parity shards left): every proof
+    validates, every payload decodes, instance 0 is bit-exact vs the oracle."""
+    torch = torch_cuda
+    f = (n - 1) // 3
+    k = n - 2 * f
+    if erase == "worst":
+        # present = parity rows k..2k-1 only (rebuilds all data + the other parity)
+        r = None
+        rb = hb.RbcBatch(n, f, device=0)
+        S = hb.shard_len(plen, k)
+        pay = np.stack([orc.gen_payload(0x48424246, i, plen) for i in range(count)])
+        payloads = torch.zeros((count, (plen + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+        payloads[:, :plen] = torch.from_numpy(pay).cuda()
+        slab = rb.alloc_slab(count, S)
+        nodes = rb.alloc_nodes(count)
+        rb.frame_encode(payloads, plen, slab)
+        rb.merkle(slab, S, nodes)
+        ref = slab[:1, :, :S].cpu().numpy()
+        present = torch.zeros((count, n), dtype=torch.uint8, device="cuda")
+        present[:, k:2 * k] = 1
+        recv = slab.clone()
+        recv[present == 0] = 0xA5
+        nodes2 = rb.alloc_nodes(count)
+        out = torch.zeros((count, (k * S + 15) // 16 * 16), dtype=torch.uint8, device="cuda")
+        plen_out = torch.zeros(count, dtype=torch.int32, device="cuda")
+        status = torch.zeros(count, dtype=torch.int32, device="cuda")
+        rb.decode(recv, S, present, nodes[:, -1, :].clone(), nodes2, out, plen_out, status)
+        torch.cuda.synchronize()
+        assert (status.cpu() == 0).all() and (plen_out.cpu() == plen).all()
+        assert torch.equal(out[:, :plen].cpu(), torch.from_numpy(pay))
+        assert torch.equal(recv, slab) and torch.equal(nodes2, nodes)
+    else:
+        r = run_pipeline(torch, n, f, plen, count, seed=0x48424246, erase_seed=2, n_erase=f)
+        assert r["ok"].all()
+        assert (r["status"] == 0).all() and (r["plen"] == plen).all()
+        assert np.array_equal(r["out"][:, :plen], r["pay"])
+        S = r["S"]
+        ref = r["slab"][:1, :, :S]
+        pay = r["pay"]
+    sh, nd = orc.send_shards(n, f, pay[0].tobytes())
+    assert np.array_equal(ref[0], sh)
