@@ -102,6 +102,8 @@ def lib():
         "hbrbc_wire_decode_batch": (ctypes.c_int, [_P, _P, _S, _P, _S, _P, _S, _P, _P, _P, _P, _P,
                                                    _P, _P, _P]),
         "hbrbc_jit_build_encode": (ctypes.c_int, [_S, _S, ctypes.c_char_p]),
+        "hbrbc_jit_encode_groups": (_S, [_S, _S]),
+        "hbrbc_jit_build_encode_group": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -116,11 +118,20 @@ def _check(code):
         raise RseError(code, lib().hbrbc_last_error().decode(errors="replace"))
 
 
-def jit_build_encode(data_shards, parity_shards, directory=None):
+def jit_build_encode(data_shards, parity_shards, directory=None, group=None):
     """Generate + compile (hiprtc, gfx950; no GPU needed) the specialised RS
-    encoder for this matrix into the code-object cache (jit.hip)."""
-    _check(lib().hbrbc_jit_build_encode(data_shards, parity_shards,
-                                        directory.encode() if directory else None))
+    encoder for this matrix into the code-object cache (jit.hip): every
+    parity-row group, or just `group`."""
+    d = directory.encode() if directory else None
+    if group is None:
+        _check(lib().hbrbc_jit_build_encode(data_shards, parity_shards, d))
+    else:
+        _check(lib().hbrbc_jit_build_encode_group(data_shards, parity_shards, group, d))
+
+
+def jit_encode_groups(data_shards, parity_shards):
+    """Number of code objects (parity-row groups) of the specialised encoder."""
+    return lib().hbrbc_jit_encode_groups(data_shards, parity_shards)
 
 
 def shard_len(payload_len, data_shards):

@@ -165,9 +165,13 @@ struct hbrbc_ctx {
     std::vector<uint8_t> matrix;  // n x k
     hipStream_t stream = nullptr;
     // specialised encoder (jit.hip) for this matrix, when its code object is available
-    hipModule_t enc_mod = nullptr;
-    hipFunction_t enc_fn = nullptr;
-    hipFunction_t fe_fn = nullptr;   // its frame+encode twin
+    // specialised encoder (jit.hip), one module per parity-row group
+    struct SpecGroup {
+        int r_lo, r_hi;
+        hipModule_t mod;
+        hipFunction_t enc, fe;       // encode / frame+encode twin
+    };
+    std::vector<SpecGroup> spec;
     int rt_spec = 2;              // parity rows per pass of the specialised encoder
     int depth_spec = 4;           // its data-row prefetch depth
     std::string enc_kind = "none";
@@ -349,8 +353,8 @@ std::string jit_dir() {
     return "jit";
 }
 
-std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth) {
-    return dir + "/" + encode_kernel_name(k, m, rt, depth, false) + "_v5.co";
+std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth, int r_lo) {
+    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) + "_v6.co";
 }
 
 // Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).
@@ -374,52 +378,79 @@ bool read_file(const std::string &path, std::vector<char> &out) {
 // Parity rows per pass of the specialised encoder: the accumulators (8 VGPRs
 // per row) plus the planes, pair XORs and load buffers must stay near 200
 // VGPRs (2 waves/SIMD) without spilling.
-int spec_row_tile(size_t m) {
+int spec_row_tile(size_t k, size_t m) {
     if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(16, atoi(e) & ~1));
-    return gf_row_tile((int)m);
+    // split matrices: 8-row passes keep each program's straight-line passes
+    // (and so its compile time) small
+    return k * m > 4096 ? 8 : gf_row_tile((int)m);
 }
 
 // Load (or, with HBRBC_JIT=1, compile and cache) the specialised encoder.
 // Any failure leaves the context on the generic bit-sliced kernel.
+void drop_spec(hbrbc_ctx *c) {
+    for (auto &g : c->spec)
+        if (g.mod) (void)hipModuleUnload(g.mod);
+    c->spec.clear();
+}
+
 void setup_spec_encoder(hbrbc_ctx *c) {
     const char *mode = getenv("HBRBC_JIT");
-    if (c->m == 0 || (mode && !std::strcmp(mode, "0")) || c->k * c->m > 8192) return;
-    c->rt_spec = spec_row_tile(c->m);
+    if (c->m == 0 || (mode && !std::strcmp(mode, "0")) || c->k * c->m > 16384) return;
+    c->rt_spec = spec_row_tile(c->k, c->m);
     c->depth_spec = spec_depth();
-    const std::string path = jit_file(jit_dir(), c->k, c->m, c->rt_spec, c->depth_spec);
-    std::vector<char> code;
-    if (!read_file(path, code)) {
-        if (!mode || std::strcmp(mode, "1")) return;
-        std::string log;
-        if (compile_encode(c->k, c->m, c->matrix.data() + c->k * c->k, c->rt_spec, c->depth_spec,
-                           code, log)) {
-            c->enc_kind = "jit-failed";
-            return;
+    for (const auto &rg : encode_groups(c->k, c->m, c->rt_spec)) {
+        const std::string path =
+            jit_file(jit_dir(), c->k, c->m, c->rt_spec, c->depth_spec, rg.first);
+        std::vector<char> code;
+        if (!read_file(path, code)) {
+            if (!mode || std::strcmp(mode, "1")) return drop_spec(c);
+            std::string log;
+            if (compile_encode(c->k, c->m, c->matrix.data() + c->k * c->k, c->rt_spec,
+                               c->depth_spec, rg.first, rg.second, code, log)) {
+                c->enc_kind = "jit-failed";
+                return drop_spec(c);
+            }
+            mkdir(jit_dir().c_str(), 0755);
+            if (FILE *f = fopen(path.c_str(), "wb")) {
+                fwrite(code.data(), 1, code.size(), f);
+                fclose(f);
+            }
         }
-        mkdir(jit_dir().c_str(), 0755);
-        if (FILE *f = fopen(path.c_str(), "wb")) {
-            fwrite(code.data(), 1, code.size(), f);
-            fclose(f);
-        }
-    }
-    if (hipModuleLoadData(&c->enc_mod, code.data()) != hipSuccess) {
-        c->enc_mod = nullptr;
-        return;
-    }
-    if (hipModuleGetFunction(&c->enc_fn, c->enc_mod,
-                             encode_kernel_name(c->k, c->m, c->rt_spec, c->depth_spec, false)
-                                 .c_str()) != hipSuccess ||
-        hipModuleGetFunction(&c->fe_fn, c->enc_mod,
-                             encode_kernel_name(c->k, c->m, c->rt_spec, fused_depth(c->depth_spec),
-                                                true)
-                                 .c_str()) != hipSuccess) {
-        (void)hipModuleUnload(c->enc_mod);
-        c->enc_mod = nullptr;
-        c->enc_fn = nullptr;
-        c->fe_fn = nullptr;
-        return;
+        hbrbc_ctx::SpecGroup g{rg.first, rg.second, nullptr, nullptr, nullptr};
+        if (hipModuleLoadData(&g.mod, code.data()) != hipSuccess) return drop_spec(c);
+        c->spec.push_back(g);
+        auto &b = c->spec.back();
+        if (hipModuleGetFunction(&b.enc, b.mod,
+                                 encode_kernel_name(c->k, c->m, c->rt_spec, c->depth_spec, false,
+                                                    rg.first)
+                                     .c_str()) != hipSuccess ||
+            hipModuleGetFunction(&b.fe, b.mod,
+                                 encode_kernel_name(c->k, c->m, c->rt_spec,
+                                                    fused_depth(c->depth_spec), true, rg.first)
+                                     .c_str()) != hipSuccess)
+            return drop_spec(c);
     }
     c->enc_kind = "specialised";
+}
+
+// Launch one group's encode (fused = frame+encode twin of group 0).
+hipError_t launch_spec_group(hbrbc_ctx *c, const hbrbc_ctx::SpecGroup &g, bool fused,
+                             uint8_t *shards, size_t shard_len, size_t shard_stride,
+                             size_t inst_stride, size_t count, const uint8_t *payloads,
+                             size_t payload_stride, size_t payload_len, hipStream_t s) {
+    uint8_t *base = shards;
+    const uint8_t *pay = payloads;
+    unsigned long ist = inst_stride, sst = shard_stride, pst = payload_stride;
+    unsigned row_bytes = (unsigned)(fused ? shard_stride : round_up(shard_len, 16));
+    unsigned P = (unsigned)payload_len, S = (unsigned)shard_len;
+    unsigned wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
+    const size_t blocks = (size_t)wpr * count;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const int npass = (g.r_hi - g.r_lo + c->rt_spec - 1) / c->rt_spec;
+    const unsigned threads = 64u * (unsigned)std::min(4, npass);
+    void *args[] = {&base, &ist, &sst, &row_bytes, &wpr, &pay, &pst, &P, &S};
+    return hipModuleLaunchKernel(fused ? g.fe : g.enc, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s,
+                                 args, nullptr);
 }
 
 std::once_flag g_default_once;
@@ -550,7 +581,7 @@ void hbrbc_coding_free(hbrbc_ctx *c) {
                       &c->st_aux3})
         b->release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    if (c->enc_mod) (void)hipModuleUnload(c->enc_mod);
+    drop_spec(c);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -622,19 +653,11 @@ int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     HB_HIP(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     StageTimer t(c, HBRBC_STAGE_ENCODE, s);
-    if (c->enc_fn) {
-        // specialised XOR network (jit.hip): same lane mapping as the bit-sliced kernel
-        uint8_t *base = shards;
-        unsigned long ist = inst_stride, sst = shard_stride;
-        unsigned row_bytes = (unsigned)(round_up(shard_len, 16));
-        unsigned wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
-        const size_t blocks = (size_t)wpr * count;
-        if (blocks > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "grid too large");
-        const int npass = (int)((c->m + c->rt_spec - 1) / c->rt_spec);
-        const unsigned threads = 64u * (unsigned)std::min(4, npass);
-        void *args[] = {&base, &ist, &sst, &row_bytes, &wpr};
-        HB_HIP(hipModuleLaunchKernel(c->enc_fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args,
-                                     nullptr));
+    if (!c->spec.empty()) {
+        // specialised XOR networks (jit.hip), one launch per parity-row group
+        for (const auto &grp : c->spec)
+            HB_HIP(launch_spec_group(c, grp, false, shards, shard_len, shard_stride, inst_stride,
+                                     count, nullptr, 0, 0, s));
         return HBRBC_OK;
     }
     GfApplyArgs g;
@@ -664,7 +687,7 @@ int hbrbc_frame_encode_batch(hbrbc_ctx *c, const uint8_t *payloads, size_t paylo
                              size_t shard_stride, size_t inst_stride, void *stream) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (count == 0) return HBRBC_OK;
-    const bool fused = c->fe_fn && shard_stride == round_up(shard_len, 16) &&
+    const bool fused = !c->spec.empty() && shard_stride == round_up(shard_len, 16) &&
                        shard_len == hbrbc_shard_len(payload_len, c->k) &&
                        payload_len <= 0x7FFFFFFFull && shard_len * c->k < 0x7FFFFFFFull;
     if (!fused) {
@@ -682,23 +705,19 @@ int hbrbc_frame_encode_batch(hbrbc_ctx *c, const uint8_t *payloads, size_t paylo
     HB_HIP(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
     StageTimer t(c, HBRBC_STAGE_ENCODE, s);
-    // frame folded into the specialised encoder (jit.hip): the data rows are
-    // written by pass 0 from the payloads, parity from the same registers
-    uint8_t *base = shards;
-    const uint8_t *pay = payloads;
-    unsigned long ist = inst_stride, sst = shard_stride, pst = payload_stride;
-    unsigned row_bytes = (unsigned)shard_stride, P = (unsigned)payload_len, S = (unsigned)shard_len;
-    unsigned wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
-    const size_t blocks = (size_t)wpr * count;
-    if (blocks > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "grid too large");
-    const int npass = (int)((c->m + c->rt_spec - 1) / c->rt_spec);
-    const unsigned threads = 64u * (unsigned)std::min(4, npass);
-    void *args[] = {&base, &ist, &sst, &row_bytes, &wpr, &pay, &pst, &P, &S};
-    HB_HIP(hipModuleLaunchKernel(c->fe_fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args,
-                                 nullptr));
+    // frame folded into the specialised encoder (jit.hip): group 0's twin
+    // writes the framed data rows and its parity rows, the fixup adds the
+    // last partial payload dword to both, and the other groups then encode
+    // from the complete data rows
+    const auto &g0 = c->spec.front();
+    HB_HIP(launch_spec_group(c, g0, true, shards, shard_len, shard_stride, inst_stride, count,
+                             payloads, payload_stride, payload_len, s));
     HB_HIP(launch_frame_fixup(payloads, payload_stride, payload_len, shards, shard_len,
-                              shard_stride, inst_stride, c->k, c->m, c->d_matrix.as<uint8_t>(),
-                              count, s));
+                              shard_stride, inst_stride, c->k, (size_t)g0.r_hi,
+                              c->d_matrix.as<uint8_t>(), count, s));
+    for (size_t i = 1; i < c->spec.size(); ++i)
+        HB_HIP(launch_spec_group(c, c->spec[i], false, shards, shard_len, shard_stride,
+                                 inst_stride, count, nullptr, 0, 0, s));
     return HBRBC_OK;
 }
 
@@ -1117,26 +1136,47 @@ int hbrbc_wire_decode_batch(hbrbc_ctx *c, const uint8_t *msgs, size_t msg_stride
 // ------------------------------------------------------ specialised encode --
 const char *hbrbc_encode_kernel(const hbrbc_ctx *c) { return c ? c->enc_kind.c_str() : "none"; }
 
-int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char *dir) {
+size_t hbrbc_jit_encode_groups(size_t data_shards, size_t parity_shards) {
+    if (data_shards == 0 || parity_shards == 0) return 0;
+    return encode_groups(data_shards, parity_shards, spec_row_tile(data_shards, parity_shards))
+        .size();
+}
+
+int hbrbc_jit_build_encode_group(size_t data_shards, size_t parity_shards, size_t group,
+                                 const char *dir) {
     if (data_shards == 0 || parity_shards == 0 || data_shards + parity_shards > 256)
         return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, data + parity <= 256");
     std::vector<uint8_t> mat;
     if (!build_matrix(data_shards, data_shards + parity_shards, mat))
         return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
-    const int rt = spec_row_tile(parity_shards), depth = spec_depth();
+    const int rt = spec_row_tile(data_shards, parity_shards), depth = spec_depth();
+    const auto groups = encode_groups(data_shards, parity_shards, rt);
+    if (group >= groups.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group,
+                                            groups.size());
     std::vector<char> code;
     std::string log;
     if (compile_encode(data_shards, parity_shards, mat.data() + data_shards * data_shards, rt,
-                       depth, code, log))
+                       depth, groups[group].first, groups[group].second, code, log))
         return fail(HBRBC_E_DEVICE, "hiprtc: %s", log.substr(0, 400).c_str());
     const std::string d = dir ? std::string(dir) : jit_dir();
     mkdir(d.c_str(), 0755);
-    const std::string path = jit_file(d, data_shards, parity_shards, rt, depth);
+    const std::string path =
+        jit_file(d, data_shards, parity_shards, rt, depth, groups[group].first);
     FILE *f = fopen(path.c_str(), "wb");
     if (!f) return fail(HBRBC_E_INVALID_ARG, "cannot write %s", path.c_str());
     const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
     fclose(f);
     return ok ? HBRBC_OK : fail(HBRBC_E_INVALID_ARG, "short write %s", path.c_str());
+}
+
+int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char *dir) {
+    const size_t n = hbrbc_jit_encode_groups(data_shards, parity_shards);
+    if (n == 0) return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1");
+    for (size_t g = 0; g < n; ++g) {
+        const int st = hbrbc_jit_build_encode_group(data_shards, parity_shards, g, dir);
+        if (st) return st;
+    }
+    return HBRBC_OK;
 }
 
 // ------------------------------------------------------------- profiling --

@@ -19,7 +19,7 @@
 // rows.  Output is bit-identical to the generic kernels (tests compare both
 // with the oracle).
 //
-// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_v5.co);
+// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_r<first row>_v6.co);
 // __graft_entry__.build() pre-generates them for the BASELINE validator
 // counts, and a context loads the file when present.  Compiling a missing
 // one at context creation is opt-in (HBRBC_JIT=1) since it takes seconds.
@@ -96,20 +96,32 @@ __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
 
 }  // namespace
 
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, bool fused) {
-    char b[96];
-    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d%s", k, m, rt, depth, fused ? "_fe" : "");
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, bool fused, int r_lo) {
+    char b[112];
+    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d%s", k, m, rt, depth, r_lo,
+             fused ? "_fe" : "");
     return b;
 }
 
+std::vector<std::pair<int, int>> encode_groups(size_t k, size_t m, int rt) {
+    // a group = one hiprtc program; bigger ones compile superlinearly slowly
+    const size_t kMaxCoefs = 4096;
+    std::vector<std::pair<int, int>> g;
+    size_t per = m;
+    if (k * m > kMaxCoefs) per = std::max<size_t>((size_t)rt, kMaxCoefs / k / rt * rt);
+    for (size_t lo = 0; lo < m; lo += per) g.push_back({(int)lo, (int)std::min(m, lo + per)});
+    return g;
+}
+
 std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
-                              bool fused) {
-    const int npass = (int)((m + rt - 1) / rt);
+                              bool fused, int r_lo, int r_hi) {
+    (void)m;
+    const int npass = (r_hi - r_lo + rt - 1) / rt;
     if (fused) depth = fused_depth(depth);  // 36 bytes per row in flight
     const int nbuf = depth + 1;
     std::ostringstream o;
     o << "\nextern \"C\" __global__ __launch_bounds__(256) void "
-      << encode_kernel_name(k, m, rt, depth, fused)
+      << encode_kernel_name(k, m, rt, depth, fused, r_lo)
       << "(uint8_t *__restrict__ base, unsigned long inst_stride, unsigned long shard_stride,\n"
          "    unsigned row_bytes, unsigned waves_per_row"
       << (fused ? ", const uint8_t *__restrict__ payloads, unsigned long payload_stride,\n"
@@ -153,8 +165,8 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
     o << "  for (int p = __builtin_amdgcn_readfirstlane(wave); p < " << npass
       << "; p += nw) {\n    switch (p) {\n";
     for (int p = 0; p < npass; ++p) {
-        const int r0 = p * rt;
-        const int rows = (int)std::min<size_t>((size_t)rt, m - (size_t)r0);
+        const int r0 = r_lo + p * rt;
+        const int rows = std::min(rt, r_hi - r0);
         // a distinct barrier opens every case, so no common prefix (the first
         // rows' loads) is hoisted above the switch and kept live across it
         o << "    case " << p << ": {\n      __asm__ volatile(\"; pass " << p
@@ -195,7 +207,7 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
                      "            const int lim_ = (int)S - (int)off - 4 * i_;\n"
                      "            x[i_] = lim_ >= 4 ? x[i_] : (lim_ <= 0 ? 0u : x[i_] & (0xFFFFFFFFu >> (8 * (4 - lim_))));\n"
                      "          }\n        }\n";
-                if (p == 0)  // pass 0 also writes the framed data row
+                if (p == 0 && r_lo == 0)  // pass 0 of group 0 also writes the framed data row
                     o << "        if (active) {\n"
                          "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[0], x[1], x[2], x[3]}, rs, off, "
                       << j << "u * sst, 0);\n"
@@ -272,14 +284,16 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
     return o.str();
 }
 
-std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth) {
-    return std::string(kPrelude) + gen_encode_kernel(k, m, parity_rows, rt, depth, false) +
-           gen_encode_kernel(k, m, parity_rows, rt, depth, true);
+std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
+                              int r_lo, int r_hi) {
+    return std::string(kPrelude) +
+           gen_encode_kernel(k, m, parity_rows, rt, depth, false, r_lo, r_hi) +
+           gen_encode_kernel(k, m, parity_rows, rt, depth, true, r_lo, r_hi);
 }
 
-int compile_encode(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
-                   std::vector<char> &code, std::string &log) {
-    const std::string src = gen_encode_source(k, m, parity_rows, rt, depth);
+int compile_encode(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth, int r_lo,
+                   int r_hi, std::vector<char> &code, std::string &log) {
+    const std::string src = gen_encode_source(k, m, parity_rows, rt, depth, r_lo, r_hi);
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "hbrbc_enc.hip", 0, nullptr, nullptr) !=
         HIPRTC_SUCCESS) {

@@ -138,7 +138,8 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(
 // The fused frame+encode kernel (jit.hip) reads the payload in whole dwords;
 // the last P & 3 payload bytes are added here: each is written into its data
 // row and, GF(2^8) being linear, c * byte is XORed into every parity row at
-// the same position (c = M[k + r][row]).  One thread per instance.
+// the same position (c = M[k + r][row]) for parity rows r < m (the rows the
+// fused launch computed).  One thread per instance.
 __global__ __launch_bounds__(kBlock) void frame_fixup_kernel(
     const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P,
     uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,

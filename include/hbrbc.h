@@ -247,6 +247,12 @@ const char *hbrbc_encode_kernel(const hbrbc_ctx *ctx);
  * default directory).  With HBRBC_JIT=1 a context compiles a missing one
  * itself; HBRBC_JIT=0 disables the specialised path. */
 int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char *dir);
+/* Large matrices are split into parity-row groups, one code object each (a
+ * program stays near 4096 coefficients, so hiprtc time stays near a minute);
+ * these build them one at a time, e.g. in parallel processes. */
+size_t hbrbc_jit_encode_groups(size_t data_shards, size_t parity_shards);
+int hbrbc_jit_build_encode_group(size_t data_shards, size_t parity_shards, size_t group,
+                                 const char *dir);
 
 /* ---- measurement hooks (bench.py) --------------------------------------- */
 /* Stage ids for the per-stage device timers. */

@@ -349,8 +349,9 @@ def test_specialised_encoder_vs_oracle(torch_cuda, monkeypatch, tmp_path, k, m, 
 def test_baseline_contexts_use_the_specialised_encoder(torch_cuda):
     """The shipped code objects (built by __graft_entry__.build) are picked up
     by the product path for the BASELINE validator counts."""
-    for n in (4, 16, 64, 128):
+    for n in (4, 16, 64, 128, 250):
         assert hb.Coding.for_validators(n).encode_kernel() == "specialised", n
+    assert hb.jit_encode_groups(84, 166) == 4   # N=250 is split over four code objects
 
 
 @pytest.mark.parametrize("n,plen,count", [(4, 0, 2), (4, 1, 2), (4, 3, 2), (4, 1024, 3), (4, 61, 2),
