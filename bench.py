@@ -278,17 +278,25 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
     import torch
     import torch.distributed as dist
 
-    from hbbft_amd.sharded import DistExchange, ShardedBroadcast, SoloExchange
+    from hbbft_amd.sharded import DistExchange, ShardedBroadcast, SoloExchange, pipelined_step
 
-    sb = ShardedBroadcast(n, count, plen, rank, world, device=local)
+    nsub = max(1, min(args.streams, count)) if world > 1 else 1
+    bounds = [(i * count) // nsub for i in range(nsub + 1)]
+    subs = [ShardedBroadcast(n, bounds[i + 1] - bounds[i], plen, rank, world, device=local)
+            for i in range(nsub)]
+    sb = subs[0]
     ex = DistExchange() if world > 1 else SoloExchange()
     g = torch.Generator(device=dev)
     g.manual_seed(0x48424246 + rank)
     pstride = (plen + 15) // 16 * 16
     payloads = torch.randint(0, 256, (count, pstride), dtype=torch.uint8, device=dev, generator=g)
+    pay_sub = [payloads[bounds[i]:bounds[i + 1]] for i in range(nsub)]
     xev = []   # (start, end) events around the two exchanges, on torch's stream
 
     def step(timed=False):
+        if nsub > 1:   # sub-batches with every exchange in flight behind compute
+            pipelined_step(subs, pay_sub, ex)
+            return
         sb.propose(payloads)
         sb.pack_value()
         a = torch.cuda.Event(enable_timing=True) if timed else None
@@ -315,12 +323,14 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
     torch.cuda.synchronize(dev)
     if not args.no_verify:
         real = len(sb.topo.validators(rank))
-        assert bool((sb.ok_v[:, :, :real] == 1).all()), "a valid Value proof was rejected"
-        assert bool((sb.status == 0).all()), "decode failed"
-        assert bool((sb.plen_out == plen).all())
-        assert torch.equal(sb.out[:, :plen], payloads[:, :plen]), "decoded payload differs"
-    sb.rb.profile(True)
-    sb.rb.profile_reset()
+        for i, s_ in enumerate(subs):
+            assert bool((s_.ok_v[:, :, :real] == 1).all()), "a valid Value proof was rejected"
+            assert bool((s_.status == 0).all()), "decode failed"
+            assert bool((s_.plen_out == plen).all())
+            assert torch.equal(s_.out[:, :plen], pay_sub[i][:, :plen]), "decoded payload differs"
+    for s_ in subs:
+        s_.rb.profile(True)
+        s_.rb.profile_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -329,13 +339,19 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
         step(timed=True)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    sb.rb.profile(False)
+    for s_ in subs:
+        s_.rb.profile(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    stages = {k: v for k, v in sb.rb.profile_read().items()}
+    stages = {}
+    for s_ in subs:
+        for st_name, (ms, cnt) in s_.rb.profile_read().items():
+            a0, c0 = stages.get(st_name, (0.0, 0))
+            stages[st_name] = (a0 + ms, c0 + cnt)
+    count_launch = count // nsub
     xms = sum(a.elapsed_time(b) for a, b in xev)
     S, k, m = sb.S, sb.rb.k, sb.rb.m
     L = (S + 1 + 135) // 136
@@ -345,8 +361,9 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
     dom = max(alg_bytes, key=lambda s_: stages[s_][0])
     dom_ms, dom_launches = stages[dom]
     per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
-    achieved = alg_bytes[dom] * count / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    perms = {"leaf_hash": count * n * L, "validate": count * (n * L + n * sb.rb.dslots)}
+    achieved = alg_bytes[dom] * count_launch / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    perms = {"leaf_hash": count_launch * n * L,
+             "validate": count_launch * (n * L + n * sb.rb.dslots)}
     valu = None
     if dom in perms:
         ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
@@ -371,7 +388,8 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
                                       sb.topo.rpg),
                        "n": n, "f": sb.topo.f, "payload_bytes": plen, "shard_len": S,
                        "instances_per_gpu": count, "global_batch": count * world,
-                       "parallelism": "validator-sharded x%d" % world},
+                       "parallelism": "validator-sharded x%d" % world,
+                       "pipelined_sub_batches": nsub},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "launch_ms": per_launch_s * 1e3, "valu": valu},

@@ -109,31 +109,41 @@ class DistExchange:
         self.rank = dist.get_rank(group)
         self.staged = dist.get_backend(group) != "nccl"
 
-    def all_to_all(self, out, inp):
-        """out[s] on this rank = inp[rank] on rank s (dim 0 = ranks)."""
+    def all_to_all(self, out, inp, async_op=False):
+        """out[s] on this rank = inp[rank] on rank s (dim 0 = ranks).  With
+        async_op (NCCL only) returns a handle; wait() makes torch's current
+        stream wait for it, so the copy overlaps whatever is queued meanwhile."""
         assert out.shape[0] == self.world and inp.shape[0] == self.world
         if self.world == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
-            return
+            return None
         if self.staged and out.is_cuda:
             o, i = out.cpu(), inp.cpu()
             self.dist.all_to_all_single(o, i, group=self.group)
             out.copy_(o)
-        else:
-            self.dist.all_to_all_single(out, inp, group=self.group)
+            return None
+        return self.dist.all_to_all_single(out, inp, group=self.group,
+                                           async_op=async_op and not self.staged)
 
-    def all_gather(self, out, inp):
+    def all_gather(self, out, inp, async_op=False):
         """out[s] = inp of rank s."""
         if self.world == 1:
             out[0].copy_(inp)
-            return
+            return None
         if self.staged:
             parts = [torch.empty_like(inp, device="cpu") for _ in range(self.world)]
             self.dist.all_gather(parts, inp.cpu(), group=self.group)
             out.copy_(torch.stack(parts))
-        else:
-            self.dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group)
+            return None
+        return self.dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group,
+                                                async_op=async_op)
+
+
+def wait_all(handles):
+    for h in handles:
+        if h is not None:
+            h.wait()
 
 
 class SoloExchange:
@@ -142,11 +152,11 @@ class SoloExchange:
 
     world, rank = 1, 0
 
-    def all_to_all(self, out, inp):
+    def all_to_all(self, out, inp, async_op=False):
         if out.data_ptr() != inp.data_ptr():
             out.copy_(inp)
 
-    def all_gather(self, out, inp):
+    def all_gather(self, out, inp, async_op=False):
         out[0].copy_(inp)
 
 
@@ -231,10 +241,12 @@ class ShardedBroadcast:
         flat[:, :n, ds * 32] = self.ndig
         pack_rows(flat, G, R, self.send_dg)
 
-    def exchange_value(self, ex):
-        ex.all_to_all(self.recv_sh, self.send_sh)
-        ex.all_to_all(self.recv_dg, self.send_dg)
-        ex.all_gather(self.roots_all, self.roots())
+    def exchange_value(self, ex, async_op=False):
+        """Value messages (+ the roots' all-gather); returns the handles."""
+        self._roots = self.roots().contiguous()   # kept alive while in flight
+        return [ex.all_to_all(self.recv_sh, self.send_sh, async_op),
+                ex.all_to_all(self.recv_dg, self.send_dg, async_op),
+                ex.all_gather(self.roots_all, self._roots, async_op)]
 
     # 3. validators validate their Values --------------------------------------
     def validate_values(self):
@@ -248,9 +260,10 @@ class ShardedBroadcast:
                               self.ok_v.view(G * C, R))
 
     # 4. Echo messages back to the proposer's rank ------------------------------
-    def exchange_echo(self, ex):
-        ex.all_to_all(self.echo_sh, self.recv_sh)
-        ex.all_to_all(self.echo_ok, self.ok_v)
+    def exchange_echo(self, ex, async_op=False):
+        """Echo messages back to the proposers' ranks; returns the handles."""
+        return [ex.all_to_all(self.echo_sh, self.recv_sh, async_op),
+                ex.all_to_all(self.echo_ok, self.ok_v, async_op)]
 
     # 5. the receiver decodes ---------------------------------------------------
     def decode(self):
@@ -269,3 +282,25 @@ class ShardedBroadcast:
         self.validate_values()
         self.exchange_echo(ex)
         self.decode()
+
+
+def pipelined_step(subs, payloads, ex):
+    """One step over several sub-batches (ShardedBroadcast objects on the same
+    rank, payloads[i] for subs[i]) with every exchange in flight while the next
+    sub-batch computes: propose all -> (Value of i overlaps propose of i+1) ->
+    validate i while Value i+1 / Echo i-1 move -> decode i while Echo i+1
+    moves.  With NCCL the collectives run on the communicator's stream and
+    handle.wait() only orders torch's current stream after them."""
+    n = len(subs)
+    hv, he = [None] * n, [None] * n
+    for i, sb in enumerate(subs):
+        sb.propose(payloads[i])
+        sb.pack_value()
+        hv[i] = sb.exchange_value(ex, async_op=True)
+    for i, sb in enumerate(subs):
+        wait_all(hv[i])
+        sb.validate_values()
+        he[i] = sb.exchange_echo(ex, async_op=True)
+    for i, sb in enumerate(subs):
+        wait_all(he[i])
+        sb.decode()

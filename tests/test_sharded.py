@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from hbbft_amd.sharded import (DistExchange, ShardedBroadcast, SoloExchange, Topology,
-                               loopback_all_to_all, pack_rows, unpack_rows)
+                               loopback_all_to_all, pack_rows, pipelined_step, unpack_rows)
 from oracle import pyoracle as orc
 
 
@@ -214,6 +214,14 @@ def _gloo_gpu_worker(rank, world, port, q):
         torch.cuda.synchronize()
         good = bool((sb.status.cpu() == 0).all()) and \
             np.array_equal(sb.out.cpu().numpy()[:, :plen], pay)
+        # the pipelined schedule over two sub-batches gives the same result
+        subs = [ShardedBroadcast(n, 2, plen, rank, world, device=0) for _ in range(2)]
+        pays = [_payloads(800 + 10 * i + rank, 2, plen, subs[i].device) for i in range(2)]
+        pipelined_step(subs, [p[1] for p in pays], DistExchange())
+        torch.cuda.synchronize()
+        for sub, (pp, _) in zip(subs, pays):
+            good = good and bool((sub.status.cpu() == 0).all()) and \
+                np.array_equal(sub.out.cpu().numpy()[:, :plen], pp)
         q.put((rank, "ok" if good else "mismatch %s" % sb.status.cpu().tolist()))
     except Exception as e:  # pragma: no cover
         q.put((rank, repr(e)))
