@@ -280,7 +280,8 @@ def run_validators(args, n, plen, count, rank, world, local, dev):
 
     from hbbft_amd.sharded import DistExchange, ShardedBroadcast, SoloExchange, pipelined_step
 
-    nsub = max(1, min(args.streams, count)) if world > 1 else 1
+    # more than one rank: 4 pipelined sub-batches unless --streams says otherwise
+    nsub = max(1, min(args.streams if args.streams > 1 else 4, count)) if world > 1 else 1
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
     subs = [ShardedBroadcast(n, bounds[i + 1] - bounds[i], plen, rank, world, device=local)
             for i in range(nsub)]
