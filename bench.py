@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
                     help="sub-batches per step, each on its own HIP stream (overlap)")
+    ap.add_argument("--own-streams", action="store_true",
+                    help="run each sub-batch on its context's own HIP stream")
     ap.add_argument("--mode", choices=["instances", "validators"], default=None,
                     help="instances: every rank runs whole instances, no collective (default "
                          "except cfg4); validators: simulated validators sharded over the ranks, "
@@ -124,7 +126,8 @@ def main():
         lo, hi = bounds[i], bounds[i + 1]
         sb = subs_rb[i]
         sb.reserve(hi - lo)
-        subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
+        subs.append((sb, (sb.own_stream() if args.own_streams else torch.cuda.Stream(dev))
+                     if nsub > 1 else main, slice(lo, hi)))
 
     def run_sub(sb, sl):
         sb.frame_encode(payloads[sl], plen, slab[sl])   # frame folded into the encoder
@@ -135,22 +138,46 @@ def main():
         sb.decode(slab[sl], S, present[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
                   status[sl])
 
+    # Sub-batch streams are joined only where the host synchronises (after the
+    # warm-up and after the timed steps): each stream runs its own sub-batch
+    # step after step, ordered by the stream alone.  After every join the
+    # streams are re-staggered by one stage (stream i starts once stream i-1
+    # has finished its frame+encode), so one sub-batch's HBM-bound stages run
+    # beside another's VALU-bound Keccak instead of in lockstep with it.
+    restagger = [True]
+
     def step():
         if nsub == 1:
             run_sub(subs[0][0], subs[0][2])
             return
-        ev = torch.cuda.Event()
-        ev.record(main)
+        first = restagger[0]
+        restagger[0] = False
+        ev = None
+        if first:
+            ev = torch.cuda.Event()
+            ev.record(main)
         for sb, st, sl in subs:
-            st.wait_event(ev)
+            if first:
+                st.wait_event(ev)
             with torch.cuda.stream(st):
-                run_sub(sb, sl)
-        for _, st, _ in subs:
-            main.wait_stream(st)
+                sb.frame_encode(payloads[sl], plen, slab[sl])
+                if first:
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                sb.merkle(slab[sl], S, nodes[sl])
+                sb.proofs(nodes[sl], digests[sl], ndig[sl])
+                sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
+                roots[sl].copy_(nodes[sl, -1, :])
+                sb.decode(slab[sl], S, present[sl], roots[sl], nodes2[sl], out[sl],
+                          plen_out[sl], status[sl])
+
+    def join():
+        torch.cuda.synchronize(dev)
+        restagger[0] = True
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    join()
     if not args.no_verify:
         assert bool((ok == 1).all()), "a valid proof was rejected"
         assert bool((status == 0).all()), "decode failed"
@@ -162,11 +189,11 @@ def main():
         sb.profile_reset()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    join()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    join()
     t1 = time.perf_counter()
     for sb in subs_rb:
         sb.profile(False)

@@ -500,6 +500,13 @@ class RbcBatch:
                                              _ptr(digests), _ptr(ndig), _ptr(roots), _ptr(variant),
                                              _ptr(status), self._stream(stream)))
 
+    def own_stream(self):
+        """The context's own HIP stream (created with the context, so the
+        contexts of one process sit on successive hardware queues) wrapped as a
+        torch stream."""
+        import torch
+        return torch.cuda.ExternalStream(lib().hbrbc_stream(self.coding.handle), device=self.device)
+
     def reserve(self, count):
         _check(lib().hbrbc_reserve(self.coding.handle, count))
 

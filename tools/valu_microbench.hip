@@ -26,8 +26,8 @@ template <int KIND>
 __global__ __launch_bounds__(256) void op_loop(uint32_t *out, int iters, uint32_t s0) {
     uint32_t a[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) a[i] = threadIdx.x * 7919u + i * 104729u + s0;
-    const uint32_t b = threadIdx.x ^ 0x5a5a5a5au, c = threadIdx.x * 3u;
+    for (int i = 0; i < 16; ++i) a[i] = (KIND == 17) ? 0u : threadIdx.x * 7919u + i * 104729u + s0;
+    const uint32_t b = threadIdx.x ^ 0x5a5a5a5au, c = threadIdx.x * 3u, z = s0 >> 31;
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -53,6 +53,11 @@ __global__ __launch_bounds__(256) void op_loop(uint32_t *out, int iters, uint32_
                     asm volatile("v_lshl_add_u64 %0, %0, 7, %1" : "+v"(*(uint64_t *)&a[i & 14]) : "v"(*(uint64_t *)&a[(i + 2) & 14]));
                 if constexpr (KIND == 14) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(a[i]));
                 if constexpr (KIND == 15) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+                // power probes: the same instructions on operands that never toggle
+                if constexpr (KIND == 16) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(z));
+                if constexpr (KIND == 17) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(a[i]));
+                if constexpr (KIND == 18) asm volatile("v_lshrrev_b32 %0, 3, %1" : "=v"(a[i]) : "v"(b));
+                if constexpr (KIND == 19) asm volatile("v_lshlrev_b32 %0, 3, %1" : "=v"(a[i]) : "v"(b));
             }
         }
     }
@@ -101,14 +106,15 @@ int main() {
     const int blocks = cus * 8 * 16;  // many full rounds of residency
     CHECK(hipMalloc(&out, (size_t)blocks * 256 * 4));
     const int iters = 64;
-    const char *names[16] = {"v_xor_b32", "v_bitop3_b32", "v_alignbit_b32(v,v)", "v_perm_b32(s,s,v)",
+    const char *names[20] = {"v_xor_b32", "v_bitop3_b32", "v_alignbit_b32(v,v)", "v_perm_b32(s,s,v)",
                              "v_and_b32", "v_lshl_or_b32", "v_alignbit_b32(s,v)", "v_perm_b32(v,v,v)",
                              "v_pk_mov_b32", "v_lshrrev_b32", "v_alignbyte_b32", "v_add_u32",
-                             "v_lshrrev_b64", "v_lshl_add_u64", "v_lshlrev_b32", "v_or3_b32"};
+                             "v_lshrrev_b64", "v_lshl_add_u64", "v_lshlrev_b32", "v_or3_b32",
+                             "v_xor_b32 (x^0)", "v_alignbit_b32 (0)", "v_lshrrev_b32 (b)", "v_lshlrev_b32 (b)"};
 #define K(n) case n: hipLaunchKernelGGL(op_loop<n>, dim3(blocks), dim3(256), 0, 0, out, iters, 1u); break
-    for (int kind = 0; kind < 16; ++kind) {
+    for (int kind = 0; kind < 20; ++kind) {
         float ms = time_ms([&] {
-            switch (kind) { K(0); K(1); K(2); K(3); K(4); K(5); K(6); K(7); K(8); K(9); K(10); K(11); K(12); K(13); K(14); K(15); }
+            switch (kind) { K(0); K(1); K(2); K(3); K(4); K(5); K(6); K(7); K(8); K(9); K(10); K(11); K(12); K(13); K(14); K(15); K(16); K(17); K(18); K(19); }
         });
         const double instr = (double)blocks * 256 * iters * 8 * 16;
         printf("%-22s %8.3f ms  %6.2f T lane-instr/s\n", names[kind], ms, instr / ms / 1e9);
