@@ -16,7 +16,7 @@ import os
 __all__ = [
     "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
     "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
-    "jit_build_encode", "WIRE_VARIANTS",
+    "jit_build_encode", "jit_file_name", "WIRE_VARIANTS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -104,6 +104,7 @@ def lib():
         "hbrbc_jit_build_encode": (ctypes.c_int, [_S, _S, ctypes.c_char_p]),
         "hbrbc_jit_encode_groups": (_S, [_S, _S]),
         "hbrbc_jit_build_encode_group": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p]),
+        "hbrbc_jit_file_name": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p, _S]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -127,6 +128,13 @@ def jit_build_encode(data_shards, parity_shards, directory=None, group=None):
         _check(lib().hbrbc_jit_build_encode(data_shards, parity_shards, d))
     else:
         _check(lib().hbrbc_jit_build_encode_group(data_shards, parity_shards, group, d))
+
+
+def jit_file_name(data_shards, parity_shards, group=0):
+    """Cache file name of one group's specialised-encoder code object."""
+    buf = ctypes.create_string_buffer(256)
+    _check(lib().hbrbc_jit_file_name(data_shards, parity_shards, group, buf, 256))
+    return buf.value.decode()
 
 
 def jit_encode_groups(data_shards, parity_shards):

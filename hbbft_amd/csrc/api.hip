@@ -1169,6 +1169,21 @@ int hbrbc_jit_build_encode_group(size_t data_shards, size_t parity_shards, size_
     return ok ? HBRBC_OK : fail(HBRBC_E_INVALID_ARG, "short write %s", path.c_str());
 }
 
+int hbrbc_jit_file_name(size_t data_shards, size_t parity_shards, size_t group, char *buf,
+                        size_t buf_len) {
+    if (data_shards == 0 || parity_shards == 0 || !buf)
+        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, a buffer");
+    const int rt = spec_row_tile(data_shards, parity_shards);
+    const auto groups = encode_groups(data_shards, parity_shards, rt);
+    if (group >= groups.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group,
+                                            groups.size());
+    const std::string f = jit_file("", data_shards, parity_shards, rt, spec_depth(),
+                                   groups[group].first).substr(1);
+    if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
+    std::memcpy(buf, f.c_str(), f.size() + 1);
+    return HBRBC_OK;
+}
+
 int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char *dir) {
     const size_t n = hbrbc_jit_encode_groups(data_shards, parity_shards);
     if (n == 0) return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1");

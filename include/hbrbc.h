@@ -253,6 +253,10 @@ int hbrbc_jit_build_encode(size_t data_shards, size_t parity_shards, const char 
 size_t hbrbc_jit_encode_groups(size_t data_shards, size_t parity_shards);
 int hbrbc_jit_build_encode_group(size_t data_shards, size_t parity_shards, size_t group,
                                  const char *dir);
+/* Cache file name (no directory) of group `group`'s code object under the
+ * current generator settings; 0 and a NUL-terminated name in buf, or an error. */
+int hbrbc_jit_file_name(size_t data_shards, size_t parity_shards, size_t group, char *buf,
+                        size_t buf_len);
 
 /* ---- measurement hooks (bench.py) --------------------------------------- */
 /* Stage ids for the per-stage device timers. */
