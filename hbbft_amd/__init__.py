@@ -115,6 +115,8 @@ def lib():
 
 
 def _check(code):
+    if code == 102:   # HBRBC_E_NO_DEVICE: no silent fallback exists
+        raise HbrbcUnavailable(lib().hbrbc_last_error().decode(errors="replace") or "no HIP device")
     if code != 0:
         raise RseError(code, lib().hbrbc_last_error().decode(errors="replace"))
 

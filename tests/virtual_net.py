@@ -1,0 +1,263 @@
+"""In-process test network for hbbft_amd.broadcast.Broadcast.
+
+TEST INFRASTRUCTURE: a restatement of hbbft_testing's `VirtualNet` crank loop
+(/root/reference/hbbft_testing/src/lib.rs:223-283 process_step, 869-884
+send_input, 908-996 crank; faulty nodes are the first f by index, 775-800)
+and of the adversaries the reference's tests/broadcast.rs uses
+(hbbft_testing/src/adversary.rs:372-450 sort_ascending / swap_random /
+sort_by_random_node, 484-531 NodeOrder / Reordering, 540-607 Random;
+tests/broadcast.rs:33-98 ProposeAdversary).  Python's `random.Random` stands
+in for the reference's seeded XorShiftRng: the schedules differ, the
+properties asserted are the reference's.
+"""
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from hbbft_amd.broadcast import Broadcast, Message  # noqa: E402
+
+
+class CrankError(AssertionError):
+    pass
+
+
+class NetMessage:
+    __slots__ = ("frm", "to", "payload")
+
+    def __init__(self, frm, payload, to):
+        self.frm, self.payload, self.to = frm, payload, to
+
+
+class Node:
+    def __init__(self, node_id, algo, faulty):
+        self.id = node_id
+        self.algo = algo
+        self.faulty = faulty
+        self.outputs = []
+        self.faults = []
+
+
+class VirtualNet:
+    def __init__(self, ids, num_faulty, make_algo, adversary, rng, message_limit=None,
+                 error_on_fault=True):
+        ids = sorted(ids)
+        assert 3 * num_faulty < len(ids)
+        self.nodes = collections.OrderedDict(
+            (i, Node(i, make_algo(i), idx < num_faulty)) for idx, i in enumerate(ids))
+        self.adversary = adversary
+        self.rng = rng
+        self.messages = collections.deque()
+        self.message_limit = message_limit
+        self.message_count = 0
+        self.crank_count = 0
+        self.error_on_fault = error_on_fault
+
+    def correct_nodes(self):
+        return [n for n in self.nodes.values() if not n.faulty]
+
+    def faulty_nodes(self):
+        return [n for n in self.nodes.values() if n.faulty]
+
+    def send_input(self, node_id, value):
+        step = self.nodes[node_id].algo.handle_input(value)
+        self.process_step(node_id, step)
+        return step
+
+    def dispatch_message(self, msg):
+        return self.nodes[msg.to].algo.handle_message(msg.frm, msg.payload)
+
+    def process_step(self, stepped_id, step):
+        """lib.rs:223-283: expand targets in node-id order, store outputs, fail
+        when a correct node blames a correct node."""
+        node = self.nodes[stepped_id]
+        for tm in step.messages:
+            if not node.faulty:
+                assert stepped_id not in tm.target.ids   # targets never name the sender
+            for to in self.nodes:
+                if to != stepped_id and tm.target.contains(to):
+                    if not node.faulty:
+                        self.message_count += 1
+                    self.messages.append(NetMessage(stepped_id, tm.message, to))
+        node.outputs.extend(step.output)
+        node.faults.extend(step.fault_log)
+        if self.error_on_fault and not node.faulty:
+            for fault in step.fault_log:
+                other = self.nodes.get(fault.node_id)
+                if other is not None and not other.faulty:
+                    raise CrankError("%r blamed correct node %r: %s"
+                                     % (stepped_id, fault.node_id, fault.kind.name))
+
+    def crank(self):
+        if self.message_limit is not None and self.message_count >= self.message_limit:
+            raise CrankError("message limit %d exceeded" % self.message_limit)
+        self.adversary.pre_crank(self)
+        if not self.messages:
+            return None
+        msg = self.messages.popleft()
+        if self.nodes[msg.to].faulty:
+            step = self.adversary.tamper(self, msg)
+        else:
+            step = self.dispatch_message(msg)
+        self.process_step(msg.to, step)
+        self.crank_count += 1
+        return msg.to, step
+
+    def crank_expect(self):
+        r = self.crank()
+        if r is None:
+            raise CrankError("queue empty before every node terminated")
+        return r
+
+
+# ---- adversaries (adversary.rs) ---------------------------------------------
+def sort_ascending(net):
+    net.messages = collections.deque(sorted(net.messages, key=lambda m: m.to))
+
+
+def swap_random(net, rng):
+    n = len(net.messages)
+    if n:
+        j = rng.randrange(n)
+        net.messages[0], net.messages[j] = net.messages[j], net.messages[0]
+
+
+def random_node(net, rng):
+    ids = list(net.nodes)
+    return ids[rng.randrange(len(ids))] if ids else None
+
+
+def sort_by_random_node(net, rng):
+    picked = random_node(net, rng)
+    if picked is not None:
+        net.messages = collections.deque(
+            sorted(net.messages, key=lambda m: (m.to != picked, m.to)))
+
+
+class NullAdversary:
+    def pre_crank(self, net):
+        pass
+
+    def tamper(self, net, msg):
+        return net.dispatch_message(msg)
+
+
+class NodeOrderAdversary(NullAdversary):
+    def pre_crank(self, net):
+        sort_ascending(net)
+
+
+class ReorderingAdversary(NullAdversary):
+    def pre_crank(self, net):
+        swap_random(net, net.rng)
+
+
+class ProposeAdversary(NullAdversary):
+    """tests/broadcast.rs:33-98: once, every faulty node proposes "Fake news"
+    through a fresh Broadcast of its own; optionally drops every other message
+    faulty nodes send."""
+
+    RANDOM_PICK, SORT_ASCENDING = 0, 1
+
+    def __init__(self, strategy, drop_messages, backend=None):
+        self.strategy = strategy
+        self.drop = drop_messages
+        self.has_sent = False
+        self.backend = backend
+
+    def pre_crank(self, net):
+        if self.strategy == self.RANDOM_PICK:
+            swap_random(net, net.rng)
+        else:
+            sort_ascending(net)
+
+    def tamper(self, net, msg):
+        step = net.dispatch_message(msg)
+        if self.drop:
+            step.messages.clear()
+        if not self.has_sent:
+            self.has_sent = True
+            for fnode in net.faulty_nodes():
+                fake = Broadcast(fnode.id, fnode.algo.validator_set(), fnode.id,
+                                 backend=self.backend).handle_input(b"Fake news")
+                step.messages.extend(fake.messages)
+        return step
+
+
+class RandomAdversary(NullAdversary):
+    """adversary.rs:540-607 (replay to a random node, inject random messages
+    from message.rs:28-50 -- whose can_decode / echo_hash samples are Ready)."""
+
+    def __init__(self, p_replay, p_inject, backend):
+        self.p_replay = p_replay
+        self.p_inject = p_inject
+        self.backend = backend
+
+    def pre_crank(self, net):
+        sort_by_random_node(net, net.rng)
+
+    def random_message(self, rng):
+        kind = rng.choice(["value", "echo", "ready", "can_decode", "echo_hash"])
+        buf = bytes(rng.randrange(256) for _ in range(32))
+        proof = self.backend.MerkleTree.from_vec([buf]).proof(0)
+        if kind == "value":
+            return Message.value(proof)
+        if kind == "echo":
+            return Message.echo(proof)
+        return Message.ready(b"r" * 32)
+
+    def tamper(self, net, msg):
+        rng = net.rng
+        if rng.random() < self.p_replay:
+            picked = random_node(net, rng)
+            if picked is not None:
+                net.messages.append(NetMessage(msg.to, msg.payload, picked))
+        while rng.random() < self.p_inject:
+            sender = msg.to
+            m = self.random_message(rng)
+            for nid in net.nodes:
+                if nid != sender:
+                    net.messages.append(NetMessage(sender, m, nid))
+        return net.dispatch_message(msg)
+
+
+def max_faulty(n):
+    """util.rs:22-25."""
+    return (n - 1) // 3
+
+
+def run_broadcast(net, value, proposer_id):
+    """tests/broadcast.rs:101-147 (test_broadcast)."""
+    proposer_faulty = net.nodes[proposer_id].faulty
+    net.send_input(proposer_id, value)
+    while not all(n.algo.terminated() for n in net.nodes.values()):
+        if proposer_faulty and not net.messages:
+            assert not net.correct_nodes()[0].outputs
+            break
+        net.crank_expect()
+    if proposer_faulty:
+        first = net.correct_nodes()[0].outputs
+        assert all(n.outputs == first for n in net.nodes.values())
+    else:
+        assert all(n.outputs == [bytes(value)] for n in net.nodes.values()), \
+            [(n.id, n.outputs) for n in net.nodes.values()]
+    return net
+
+
+def broadcast_different_sizes(new_adversary, value, rng, backend, sizes=None):
+    """tests/broadcast.rs:149-185: N in 1..5, rand[6,20), rand[30,50); f =
+    max_faulty(N) faulty nodes (the first f), random proposer."""
+    if sizes is None:
+        sizes = list(range(1, 6)) + [rng.randrange(6, 20), rng.randrange(30, 50)]
+    nets = []
+    for size in sizes:
+        nf = max_faulty(size)
+        proposer = rng.randrange(size)
+        ids = list(range(size))
+        net = VirtualNet(ids, nf, lambda i: Broadcast(i, ids, proposer, backend=backend),
+                         new_adversary(), rng, message_limit=10_000 * size)
+        nets.append(run_broadcast(net, value, proposer))
+    return nets
