@@ -77,8 +77,8 @@ def test_no_cpu_fallback_without_gpu():
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present")
-    with pytest.raises(hb.RseError) as e:
-        hb.Coding(4, 2)
-    assert e.value.code == 102  # NoDevice: fails loudly, never computes on the host
+    with pytest.raises(hb.HbrbcUnavailable):   # HBRBC_E_NO_DEVICE (102): fails loudly,
+        hb.Coding(4, 2)                         # never computes on the host
+    assert hb.lib().hbrbc_coding_new(4, 2, -1, ctypes.byref(ctypes.c_void_p())) == 102
     with pytest.raises(hb.HbrbcUnavailable):
         hb.RbcBatch(16)

@@ -294,3 +294,15 @@ def test_trivial_coding_single_node(backend):
         net = vn.VirtualNet(ids, 0, lambda i: Broadcast(i, ids, n - 1, backend=backend),
                             vn.NullAdversary(), random.Random(n))
         vn.run_broadcast(net, b"trivial", n - 1)
+
+
+def test_default_backend_has_no_cpu_fallback():
+    """The product backend is libhbrbc.so: without a GPU, Broadcast::new fails loudly."""
+    import torch
+
+    import hbbft_amd
+    if torch.cuda.is_available():
+        assert Broadcast(0, range(4), 0).coding.encode_kernel()   # HIP context
+        return
+    with pytest.raises(hbbft_amd.HbrbcUnavailable):
+        Broadcast(0, range(4), 0)
