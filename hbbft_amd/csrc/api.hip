@@ -354,7 +354,7 @@ std::string jit_dir() {
 }
 
 std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth, int r_lo) {
-    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) + "_v6.co";
+    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) + "_v8.co";
 }
 
 // Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).

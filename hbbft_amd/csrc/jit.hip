@@ -12,6 +12,9 @@
 // network written out for every (parity row, data row), accumulated with
 // three-input XORs (v_bitop3): about 2.25 VALU per plane per coefficient
 // against ~4 XORs + branches in the generic kernel, and no branches at all.
+// Passes of at most 8 rows use a nibble-subset network instead (one VALU per
+// plane per coefficient, gen_nibble_network); at 14-row passes its longer
+// live ranges cost occupancy and it measured slower (5.7 -> 9.0 ms, cfg3).
 //
 // Layout and lane mapping are those of gf_bitslice_kernel: a lane owns 32
 // consecutive byte positions of every row; a workgroup holds up to 4 waves
@@ -19,7 +22,7 @@
 // rows.  Output is bit-identical to the generic kernels (tests compare both
 // with the oracle).
 //
-// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_r<first row>_v6.co);
+// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_r<first row>_v8.co);
 // __graft_entry__.build() pre-generates them for the BASELINE validator
 // counts, and a context loads the file when present.  Compiling a missing
 // one at context creation is opt-in (HBRBC_JIT=1) since it takes seconds.
@@ -93,6 +96,68 @@ __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
     }
 }
 )";
+
+// Nibble-subset XOR network of data row j for parity rows r0..r0+rows-1:
+// output plane q of c*x is the XOR of a low-nibble subset (planes 0-3) and a
+// high-nibble subset (planes 4-7) of the input planes.  The subset XORs used
+// by this data row are built once (<= 11 + 11 ops) and shared by every row of
+// the pass; each accumulator then takes exactly one op.  Fewer VALU than the
+// pairwise network but more values live across the row, so it is used for
+// short passes only (rt <= 8, the split N = 250 programs: encode 16.9 ->
+// 15.0 ms per 1024 instances; at rt 14 it costs 2 waves/SIMD of occupancy).
+void gen_nibble_network(std::ostringstream &o, size_t k, const uint8_t *parity_rows, int r0,
+                        int rows, size_t j) {
+    std::vector<std::pair<int, int>> tgt((size_t)rows * 8, {0, 0});
+    bool used[2][16] = {};
+    for (int t = 0; t < rows; ++t) {
+        const uint8_t c = parity_rows[(size_t)(r0 + t) * k + j];
+        if (!c) continue;
+        uint8_t col[8];
+        for (int q = 0; q < 8; ++q) col[q] = gf_mul_host(c, (uint8_t)(1u << q));
+        for (int q = 0; q < 8; ++q) {
+            int lo = 0, hi = 0;
+            for (int pp = 0; pp < 4; ++pp) lo |= ((col[pp] >> q) & 1) << pp;
+            for (int pp = 4; pp < 8; ++pp) hi |= ((col[pp] >> q) & 1) << (pp - 4);
+            tgt[(size_t)t * 8 + q] = {lo, hi};
+            used[0][lo] = used[1][hi] = true;
+        }
+    }
+    // a single plane is x[] itself; 2 / 3 planes one XOR / bitop3 of planes;
+    // 4 planes fold the {0,1} subset
+    auto sname = [](int h, int s) {
+        if (__builtin_popcount(s) == 1) return "x[" + std::to_string(4 * h + __builtin_ctz(s)) + "]";
+        return std::string(h ? "h" : "l") + std::to_string(s);
+    };
+    for (int h = 0; h < 2; ++h) {
+        if (used[h][15]) used[h][3] = true;
+        for (int s = 3; s < 16; ++s) {
+            if (!used[h][s] || __builtin_popcount(s) < 2) continue;
+            int pl[4], np = 0;
+            for (int b = 0; b < 4; ++b)
+                if (s >> b & 1) pl[np++] = 4 * h + b;
+            o << "        const uint32_t " << sname(h, s) << " = ";
+            if (np == 2)
+                o << "x[" << pl[0] << "] ^ x[" << pl[1] << "];\n";
+            else if (np == 3)
+                o << "__builtin_amdgcn_bitop3_b32(x[" << pl[0] << "], x[" << pl[1] << "], x[" << pl[2]
+                  << "], 0x96);\n";
+            else
+                o << "__builtin_amdgcn_bitop3_b32(" << sname(h, 3) << ", x[" << 4 * h + 2 << "], x["
+                  << 4 * h + 3 << "], 0x96);\n";
+        }
+    }
+    for (int t = 0; t < rows; ++t)
+        for (int q = 0; q < 8; ++q) {
+            const auto lh = tgt[(size_t)t * 8 + q];
+            const std::string acc = "a[" + std::to_string(t) + "][" + std::to_string(q) + "]";
+            if (lh.first && lh.second)
+                o << "        " << acc << " = __builtin_amdgcn_bitop3_b32(" << acc << ", "
+                  << sname(0, lh.first) << ", " << sname(1, lh.second) << ", 0x96);\n";
+            else if (lh.first || lh.second)
+                o << "        " << acc << " ^= " << (lh.first ? sname(0, lh.first) : sname(1, lh.second))
+                  << ";\n";
+        }
+}
 
 }  // namespace
 
@@ -220,6 +285,12 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
                 o << "      { const u32x4 hh = full ? h[" << cur << "] : (u32x4)(0u);\n"
                   << "        uint32_t x[8] = {" << lc << "[0], " << lc << "[1], " << lc << "[2], " << lc
                   << "[3], hh[0], hh[1], hh[2], hh[3]};\n        hb_tr(x);\n";
+            }
+            if (rt <= 8) {   // short passes: the nibble-subset network (below)
+                gen_nibble_network(o, k, parity_rows, r0, rows, j);
+                o << "        for (int t_ = 0; t_ < " << rows << "; ++t_) for (int q_ = 0; q_ < 8; ++q_) "
+                     "__asm__ volatile(\"\" : \"+v\"(a[t_][q_]));\n      }\n";
+                continue;
             }
             // Term lists of every (row, plane): output plane q of c*x is the
             // XOR of the planes p with bit q of c*2^p set.  Terms are paired in
