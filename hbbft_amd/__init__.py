@@ -16,7 +16,7 @@ import os
 __all__ = [
     "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
     "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
-    "jit_build_encode", "jit_file_name", "WIRE_VARIANTS",
+    "jit_build_encode", "jit_file_name", "WIRE_VARIANTS", "validate_proofs", "VALIDATE_STATS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -265,16 +265,26 @@ class Coding:
 class Proof:
     """`Proof<T>` (merkle.rs:72-78); field order value, index, digests, root_hash."""
 
-    __slots__ = ("_value", "_index", "_digests", "_root")
+    __slots__ = ("_value", "_index", "_digests", "_root", "_valid")
 
     def __init__(self, value, index, digests, root_hash):
         self._value = bytes(value)
         self._index = int(index)
         self._digests = [bytes(d) for d in digests]
         self._root = bytes(root_hash)
+        self._valid = {}   # n -> result: validate is a pure function of the proof
 
     def validate(self, n):
-        """`Proof::validate(n)` (merkle.rs:83-103), on the GPU."""
+        """`Proof::validate(n)` (merkle.rs:83-103), on the GPU.  One result per
+        (proof, n): a proof delivered to many receivers is hashed once, here or
+        in a batch by `validate_proofs`."""
+        r = self._valid.get(n)
+        if r is None:
+            r = self._valid[n] = self._validate_one(n)
+            VALIDATE_STATS["single"] += 1
+        return r
+
+    def _validate_one(self, n):
         v = _as_buffer(self._value) if self._value else None
         dig = b"".join(self._digests)
         d = _as_buffer(dig) if dig else None
@@ -308,6 +318,66 @@ class Proof:
     def __repr__(self):
         return "Proof(index=%d, root=%s, %d digests)" % (self._index, self._root.hex()[:10],
                                                          len(self._digests))
+
+
+VALIDATE_STATS = {"single": 0, "batched": 0, "launches": 0}
+_VALIDATE_CTX = {}
+
+
+def validate_proofs(proofs, n, device=0):
+    """`Proof::validate(n)` for many proofs at once: one hbrbc_validate_batch
+    launch per distinct value length (normally one: every shard of a
+    broadcast has the same length).  Results are memoised on each Proof, so
+    the state machine's own `validate` calls then cost nothing.  Proofs that
+    do not fit the batched layout (empty value, more digests than a tree over
+    n leaves has levels) take the per-call path."""
+    import numpy as np
+    import torch
+    todo, seen = [], set()
+    for p in proofs:
+        if n not in p._valid and id(p) not in seen:
+            seen.add(id(p))
+            todo.append(p)
+    ds = max_proof_len(n)
+    groups = {}
+    for p in todo:
+        if not p._value or len(p._digests) > ds or p._index > 0xFFFFFFFF:
+            p.validate(n)
+        else:
+            groups.setdefault(len(p._value), []).append(p)
+    if not groups:
+        return
+    ctx = _VALIDATE_CTX.get(device)
+    if ctx is None:
+        with torch.cuda.device(device):
+            ctx = _VALIDATE_CTX[device] = Coding(1, 0, device)
+    dev = torch.device("cuda", device)
+    for L, ps in groups.items():
+        cnt, stride = len(ps), (L + 15) // 16 * 16
+        vals = np.zeros((cnt, 1, stride), np.uint8)
+        dig = np.zeros((cnt, 1, max(ds, 1), 32), np.uint8)
+        ndig = np.zeros((cnt, 1), np.uint8)
+        roots = np.zeros((cnt, 32), np.uint8)
+        idx = np.zeros((cnt, 1), np.uint32)
+        for i, p in enumerate(ps):
+            vals[i, 0, :L] = np.frombuffer(p._value, np.uint8)
+            for d, dg in enumerate(p._digests):
+                dig[i, 0, d] = np.frombuffer(dg, np.uint8)
+            ndig[i, 0] = len(p._digests)
+            roots[i] = np.frombuffer(p._root, np.uint8)
+            idx[i, 0] = p._index
+        t = [torch.from_numpy(a).to(dev) for a in (vals, dig, ndig, roots, idx.view(np.int32))]
+        ok = torch.zeros((cnt, 1), dtype=torch.uint8, device=dev)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _check(lib().hbrbc_validate_batch(ctx.handle, t[0].data_ptr(), L, t[0].stride(1),
+                                          t[0].stride(0), 1, t[4].data_ptr(), t[1].data_ptr(),
+                                          t[2].data_ptr(), t[3].data_ptr(), t[3].stride(0), n, cnt,
+                                          ok.data_ptr(), stream))
+        res = ok.cpu().numpy()[:, 0]
+        for p, r in zip(ps, res):
+            p._valid[n] = bool(r)
+        VALIDATE_STATS["batched"] += cnt
+        VALIDATE_STATS["launches"] += 1
 
 
 class MerkleTree:

@@ -17,7 +17,7 @@ import enum
 import struct
 
 __all__ = ["ValidatorSet", "Target", "TargetedMessage", "Message", "Fault", "FaultKind", "Step",
-           "BroadcastError", "ErrorKind", "Broadcast"]
+           "BroadcastError", "ErrorKind", "Broadcast", "prevalidate"]
 
 
 # --------------------------------------------------------------------------
@@ -512,3 +512,17 @@ class Broadcast:
 
     def __repr__(self):
         return "%r Broadcast(%r)" % (self.our_id, self.proposer_id)
+
+
+def prevalidate(messages, n, backend=None):
+    """Validate the proofs of many pending Value / Echo messages (of any number
+    of Broadcast instances over n validators) in one batched launch before
+    they are delivered.  `Proof::validate` is a pure function of the proof, so
+    the results, memoised on each Proof, are exactly what every receiver's
+    `validate_proof` (broadcast.rs:604-606) would compute; the receiver's
+    index check stays in the state machine."""
+    be = backend if backend is not None else _default_backend()
+    fn = getattr(be, "validate_proofs", None)
+    if fn is not None:
+        fn([m.payload for m in messages if m.kind <= Message.ECHO], n)
+

@@ -56,18 +56,30 @@ class Coding:
                 shards[i] = out[i].tobytes()
 
 
+STATS = {"single": 0, "batched": 0, "launches": 0}
+
+
 class Proof:
-    __slots__ = ("_value", "_index", "_digests", "_root")
+    __slots__ = ("_value", "_index", "_digests", "_root", "_valid")
 
     def __init__(self, value, index, digests, root_hash):
         self._value = bytes(value)
         self._index = int(index)
         self._digests = [bytes(d) for d in digests]
         self._root = bytes(root_hash)
+        self._valid = {}
 
     def validate(self, n):
+        r = self._valid.get(n)
+        if r is None:
+            r = self._valid[n] = self._check(n)
+            STATS["single"] += 1
+        return r
+
+    def _check(self, n):
         dig = np.frombuffer(b"".join(self._digests), np.uint8).reshape(-1, 32)
         return orc.proof_validate(self._value, self._index, dig, self._root, n)
+
 
     def index(self):
         return self._index
@@ -84,6 +96,16 @@ class Proof:
     def __eq__(self, other):
         return (self._value == other._value and self._index == other._index and
                 self._digests == other._digests and self._root == other._root)
+
+
+def validate_proofs(proofs, n):
+    """Checker twin of hbbft_amd.validate_proofs (one 'launch' per call)."""
+    todo = {id(p): p for p in proofs if n not in p._valid}
+    for p in todo.values():
+        p._valid[n] = p._check(n)
+    if todo:
+        STATS["batched"] += len(todo)
+        STATS["launches"] += 1
 
 
 class MerkleTree:

@@ -306,3 +306,41 @@ def test_default_backend_has_no_cpu_fallback():
         return
     with pytest.raises(hbbft_amd.HbrbcUnavailable):
         Broadcast(0, range(4), 0)
+
+
+def _validate_stats(backend):
+    return getattr(backend, "VALIDATE_STATS", None) or backend.STATS
+
+
+def test_lockstep_batched_validation(backend):
+    """Several networks cranked in lockstep with their pending proofs validated
+    in batched launches (f2): every node's outputs and fault log equal the
+    one-network-at-a-time run of the same seeds, under the random adversary."""
+    sizes = [4, 7, 10, 16, 16, 31]
+
+    def make(i, size):
+        rng = random.Random(1000 + i)
+        proposer = rng.randrange(size)
+        ids = list(range(size))
+        net = vn.VirtualNet(ids, vn.max_faulty(size),
+                            lambda j: Broadcast(j, ids, proposer, backend=backend),
+                            vn.RandomAdversary(0.2, 0.2, backend), rng, message_limit=10_000 * size)
+        return net, b"lockstep %d" % i, proposer
+
+    seq = [make(i, s) for i, s in enumerate(sizes)]
+    for net, value, proposer in seq:
+        vn.run_broadcast(net, value, proposer)
+    st = _validate_stats(backend)
+    before = dict(st)
+    lock = [make(i, s) for i, s in enumerate(sizes)]
+    vn.run_lockstep(lock, backend)
+    for (a, _, _), (b, _, _) in zip(seq, lock):
+        for na, nb in zip(a.nodes.values(), b.nodes.values()):
+            assert na.outputs == nb.outputs
+            assert [(f.node_id, f.kind) for f in na.faults] == [(f.node_id, f.kind) for f in nb.faults]
+        assert a.crank_count == b.crank_count
+    launches = st["launches"] - before["launches"]
+    batched = st["batched"] - before["batched"]
+    assert launches > 0 and batched > launches      # several proofs per launch
+    assert st["single"] - before["single"] < batched  # only adversary-injected proofs go alone
+

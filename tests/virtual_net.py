@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from hbbft_amd.broadcast import Broadcast, Message  # noqa: E402
+from hbbft_amd.broadcast import Broadcast, Message, prevalidate  # noqa: E402
 
 
 class CrankError(AssertionError):
@@ -55,6 +55,7 @@ class VirtualNet:
         self.message_count = 0
         self.crank_count = 0
         self.error_on_fault = error_on_fault
+        self.pending = []   # Value / Echo messages queued since the last batched validation
 
     def correct_nodes(self):
         return [n for n in self.nodes.values() if not n.faulty]
@@ -75,6 +76,8 @@ class VirtualNet:
         when a correct node blames a correct node."""
         node = self.nodes[stepped_id]
         for tm in step.messages:
+            if tm.message.kind <= Message.ECHO:
+                self.pending.append(tm.message)
             if not node.faulty:
                 assert stepped_id not in tm.target.ids   # targets never name the sender
             for to in self.nodes:
@@ -235,16 +238,53 @@ def run_broadcast(net, value, proposer_id):
     net.send_input(proposer_id, value)
     while not all(n.algo.terminated() for n in net.nodes.values()):
         if proposer_faulty and not net.messages:
-            assert not net.correct_nodes()[0].outputs
             break
         net.crank_expect()
-    if proposer_faulty:
+    return check_outcome(net, value, proposer_id)
+
+
+def check_outcome(net, value, proposer_id):
+    """The assertions of tests/broadcast.rs:127-146."""
+    if net.nodes[proposer_id].faulty:
         first = net.correct_nodes()[0].outputs
         assert all(n.outputs == first for n in net.nodes.values())
     else:
         assert all(n.outputs == [bytes(value)] for n in net.nodes.values()), \
             [(n.id, n.outputs) for n in net.nodes.values()]
     return net
+
+
+def run_lockstep(items, backend):
+    """Many broadcast networks cranked in lockstep, one crank per network per
+    round.  Before every round the Value / Echo proofs all networks queued
+    since the previous round are validated together, one batched launch per
+    tree size (hbbft_amd.broadcast.prevalidate); the state machines then find
+    every result memoised.  Each network's schedule depends only on its own
+    RNG and state, so outcomes equal those of `run_broadcast`.
+    items: [(net, value, proposer)]."""
+    for net, value, proposer in items:
+        net.send_input(proposer, value)
+    live = list(items)
+    while live:
+        by_n = {}
+        for net, _, _ in live:
+            by_n.setdefault(len(net.nodes), []).extend(net.pending)
+            net.pending.clear()
+        for n, msgs in by_n.items():
+            prevalidate(msgs, n, backend)
+        nxt = []
+        for it in live:
+            net, _, proposer = it
+            if all(nd.algo.terminated() for nd in net.nodes.values()):
+                continue
+            if net.nodes[proposer].faulty and not net.messages:
+                continue
+            net.crank_expect()
+            nxt.append(it)
+        live = nxt
+    for net, value, proposer in items:
+        check_outcome(net, value, proposer)
+    return [it[0] for it in items]
 
 
 def broadcast_different_sizes(new_adversary, value, rng, backend, sizes=None):
