@@ -20,7 +20,7 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhbrbc.so")
+LIB_PATH = os.environ.get("HBRBC_LIB") or os.path.join(_HERE, "libhbrbc.so")  # A/B builds
 
 STATUS_NAMES = {
     0: "Ok", 1: "TooFewShards", 2: "TooManyShards", 3: "TooFewDataShards",
