@@ -17,6 +17,7 @@ __all__ = [
     "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
     "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
     "jit_build_encode", "jit_file_name", "WIRE_VARIANTS", "validate_proofs", "VALIDATE_STATS",
+    "send_shards_batch", "SEND_STATS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -602,3 +603,54 @@ class RbcBatch:
         cnt = (ctypes.c_uint64 * len(STAGES))()
         _check(lib().hbrbc_profile_read(self.coding.handle, ms, cnt))
         return {STAGES[i]: (ms[i], cnt[i]) for i in range(len(STAGES))}
+
+
+# --------------------------------------------------------------------------
+# Epoch batching: every proposer's send_shards in one pass
+# --------------------------------------------------------------------------
+SEND_STATS = {"trees": 0, "launches": 0}
+_SEND_BATCH = {}
+
+
+def send_shards_batch(items, device=0):
+    """The proposer half of `Broadcast::send_shards` (broadcast.rs:170-225:
+    BE32 length prefix, zero pad to N shards of ceil((P+4)/k) bytes, encode,
+    `MerkleTree::from_vec`) for many proposals at once, e.g. the N
+    contributions of one Subset / HoneyBadger epoch (subset/proposal_state.rs
+    :69-113, honey_badger/epoch_state.rs:223-236), or many epochs.
+    items: [(n, value bytes)].  Proposals with the same validator count and
+    payload length share one frame+encode and one tree launch
+    (hbrbc_frame_encode_batch, hbrbc_merkle_batch); returns one `MerkleTree`
+    per item, equal to the per-call from_vec over the encoded shards."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        raise HbrbcUnavailable("no GPU visible: the RBC path has no CPU fallback")
+    out = [None] * len(items)
+    groups = {}
+    for i, (n, value) in enumerate(items):
+        groups.setdefault((int(n), len(value)), []).append(i)
+    dev = torch.device("cuda", device)
+    for (n, plen), idx in groups.items():
+        rb = _SEND_BATCH.get((n, device))
+        if rb is None:
+            rb = _SEND_BATCH[(n, device)] = RbcBatch(n, device=device)
+        count, S = len(idx), shard_len(plen, rb.k)
+        pay = np.zeros((count, max(16, (plen + 15) // 16 * 16)), np.uint8)
+        for r, i in enumerate(idx):
+            if plen:
+                pay[r, :plen] = np.frombuffer(bytes(items[i][1]), np.uint8)
+        payloads = torch.from_numpy(pay).to(dev)
+        slab = rb.alloc_slab(count, S)
+        nodes = rb.alloc_nodes(count)
+        if rb.m:
+            rb.frame_encode(payloads, plen, slab)
+        else:   # Coding::Trivial (N <= 3): no parity
+            rb.frame(payloads, plen, slab)
+        rb.merkle(slab, S, nodes)
+        sl, nd = slab.cpu().numpy(), nodes.cpu().numpy()
+        for r, i in enumerate(idx):
+            out[i] = MerkleTree([sl[r, j, :S].tobytes() for j in range(n)], nd[r].copy())
+        SEND_STATS["trees"] += count
+        SEND_STATS["launches"] += 1
+    return out

@@ -17,7 +17,7 @@ import enum
 import struct
 
 __all__ = ["ValidatorSet", "Target", "TargetedMessage", "Message", "Fault", "FaultKind", "Step",
-           "BroadcastError", "ErrorKind", "Broadcast", "prevalidate"]
+           "BroadcastError", "ErrorKind", "Broadcast", "prevalidate", "broadcast_many"]
 
 
 # --------------------------------------------------------------------------
@@ -277,14 +277,15 @@ class Broadcast:
     def validator_set(self):
         return self.val_set
 
-    def broadcast(self, value):
-        """broadcast.rs:123-137."""
+    def broadcast(self, value, _mtree=None):
+        """broadcast.rs:123-137.  `_mtree`: the tree of this value's shards,
+        already built by `broadcast_many`."""
         if self.our_id != self.proposer_id:
             raise BroadcastError(ErrorKind.InstanceCannotPropose)
         if self.value_sent:
             raise BroadcastError(ErrorKind.MultipleInputs)
         self.value_sent = True
-        proof, step = self._send_shards(bytes(value))
+        proof, step = self._send_shards(bytes(value), _mtree)
         return step.join(self._handle_value(self.our_id, proof))
 
     def handle_message(self, sender_id, message):
@@ -303,17 +304,18 @@ class Broadcast:
         return self._handle_echo_hash(sender_id, message.payload)
 
     # -- proposer ---------------------------------------------------------------
-    def _send_shards(self, value):
+    def _send_shards(self, value, mtree=None):
         """broadcast.rs:170-225: BE32 length prefix, shard_len = ceil(len/k),
         zero pad to (k+m) shards, encode parity in place, tree, one proof per
         validator."""
-        k, m = self._k, self._m
-        framed = struct.pack(">I", len(value) & 0xFFFFFFFF) + value
-        shard_len = (len(framed) + k - 1) // k
-        buf = bytearray(framed) + bytearray(shard_len * (k + m) - len(framed))
-        shards = [bytearray(buf[i * shard_len:(i + 1) * shard_len]) for i in range(k + m)]
-        self.coding.encode(shards)
-        mtree = self._be.MerkleTree.from_vec([bytes(s) for s in shards])
+        if mtree is None:
+            k, m = self._k, self._m
+            framed = struct.pack(">I", len(value) & 0xFFFFFFFF) + value
+            shard_len = (len(framed) + k - 1) // k
+            buf = bytearray(framed) + bytearray(shard_len * (k + m) - len(framed))
+            shards = [bytearray(buf[i * shard_len:(i + 1) * shard_len]) for i in range(k + m)]
+            self.coding.encode(shards)
+            mtree = self._be.MerkleTree.from_vec([bytes(s) for s in shards])
         assert self.val_set.num() == len(mtree.values())
         step = Step()
         result = None
@@ -526,3 +528,22 @@ def prevalidate(messages, n, backend=None):
     if fn is not None:
         fn([m.payload for m in messages if m.kind <= Message.ECHO], n)
 
+
+def broadcast_many(inputs, backend=None):
+    """`Broadcast::broadcast` (broadcast.rs:123-137) of many proposer instances
+    at once -- the N contributions of a Subset / HoneyBadger epoch
+    (subset/proposal_state.rs:69-113) or several epochs.
+    inputs: [(Broadcast, value)] -> [Step], in order.  The proposers' framing,
+    encode and tree go through the backend's `send_shards_batch` (one launch
+    per validator count and payload length); each instance then sends its
+    proofs exactly as `broadcast` does.  Error checks stay per instance and
+    come first, as in `broadcast`."""
+    be = backend if backend is not None else _default_backend()
+    fn = getattr(be, "send_shards_batch", None)
+    todo = [(bc, bytes(v)) for bc, v in inputs
+            if bc.our_id == bc.proposer_id and not bc.value_sent]
+    trees = {}
+    if fn is not None and todo:
+        for (bc, v), t in zip(todo, fn([(bc.val_set.num(), v) for bc, v in todo])):
+            trees[id(bc)] = t
+    return [bc.broadcast(v, trees.get(id(bc))) for bc, v in inputs]

@@ -354,7 +354,7 @@ std::string jit_dir() {
 }
 
 std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth, int r_lo) {
-    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) + "_v8.co";
+    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) + "_v9.co";
 }
 
 // Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).
@@ -433,6 +433,12 @@ void setup_spec_encoder(hbrbc_ctx *c) {
     c->enc_kind = "specialised";
 }
 
+// HBRBC_SPEC_SPLIT=1: launch the specialised encoder pass by pass.
+bool spec_pass_split() {
+    const char *e = getenv("HBRBC_SPEC_SPLIT");
+    return e && !std::strcmp(e, "1");
+}
+
 // Launch one group's encode (fused = frame+encode twin of group 0).
 hipError_t launch_spec_group(hbrbc_ctx *c, const hbrbc_ctx::SpecGroup &g, bool fused,
                              uint8_t *shards, size_t shard_len, size_t shard_stride,
@@ -447,10 +453,24 @@ hipError_t launch_spec_group(hbrbc_ctx *c, const hbrbc_ctx::SpecGroup &g, bool f
     const size_t blocks = (size_t)wpr * count;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const int npass = (g.r_hi - g.r_lo + c->rt_spec - 1) / c->rt_spec;
-    const unsigned threads = 64u * (unsigned)std::min(4, npass);
-    void *args[] = {&base, &ist, &sst, &row_bytes, &wpr, &pay, &pst, &P, &S};
-    return hipModuleLaunchKernel(fused ? g.fe : g.enc, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s,
-                                 args, nullptr);
+    int p_only = -1;
+    void *args_e[] = {&base, &ist, &sst, &row_bytes, &wpr, &p_only};
+    void *args_f[] = {&base, &ist, &sst, &row_bytes, &wpr, &pay, &pst, &P, &S, &p_only};
+    void **args = fused ? args_f : args_e;
+    if (!spec_pass_split()) {
+        const unsigned threads = 64u * (unsigned)std::min(4, npass);
+        return hipModuleLaunchKernel(fused ? g.fe : g.enc, (unsigned)blocks, 1, 1, threads, 1, 1, 0,
+                                     s, args, nullptr);
+    }
+    // one launch per pass, one wave per workgroup: every wave on the chip
+    // runs the same pass's code (the three-pass N = 64 program is 151 KB of
+    // straight-line code, more than the instruction cache a CU pair shares)
+    for (p_only = 0; p_only < npass; ++p_only) {
+        const hipError_t e = hipModuleLaunchKernel(fused ? g.fe : g.enc, (unsigned)blocks, 1, 1, 64u,
+                                                   1, 1, 0, s, args, nullptr);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 std::once_flag g_default_once;

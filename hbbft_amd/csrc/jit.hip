@@ -22,7 +22,7 @@
 // rows.  Output is bit-identical to the generic kernels (tests compare both
 // with the oracle).
 //
-// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_r<first row>_v8.co);
+// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_r<first row>_v9.co);
 // __graft_entry__.build() pre-generates them for the BASELINE validator
 // counts, and a context loads the file when present.  Compiling a missing
 // one at context creation is opt-in (HBRBC_JIT=1) since it takes seconds.
@@ -191,7 +191,7 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
          "    unsigned row_bytes, unsigned waves_per_row"
       << (fused ? ", const uint8_t *__restrict__ payloads, unsigned long payload_stride,\n"
                   "    unsigned P, unsigned S" : "")
-      << ") {\n"
+      << ", int p_only) {\n"
          "  const unsigned long inst = blockIdx.x / waves_per_row;\n"
          "  const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);\n"
          "  const unsigned chunk = (blockIdx.x - (unsigned)inst * waves_per_row) * 64u + (threadIdx.x & 63u);\n"
@@ -227,8 +227,14 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
              "Q0 = __builtin_amdgcn_raw_buffer_load_b128(pr, a_, 0, 0); "
              "Q1 = __builtin_amdgcn_raw_buffer_load_b128(pr, a_ + 16u, 0, 0); "
              "Q2 = __builtin_amdgcn_raw_buffer_load_b32(pr, a_ + 32u, 0, 0); }\n";
-    o << "  for (int p = __builtin_amdgcn_readfirstlane(wave); p < " << npass
-      << "; p += nw) {\n    switch (p) {\n";
+    // p_only >= 0: this launch runs that one pass with one wave per workgroup
+    // (the host launches the passes one after another, so every wave on a CU
+    // runs the same straight-line code); p_only < 0: wave w runs passes w,
+    // w + nw, ... of the same byte positions
+    o << "  const int p_lo = p_only >= 0 ? p_only : __builtin_amdgcn_readfirstlane(wave);\n"
+         "  const int p_hi = p_only >= 0 ? p_only + 1 : " << npass << ";\n"
+         "  const int p_st = p_only >= 0 ? 1 : nw;\n"
+         "  for (int p = p_lo; p < p_hi; p += p_st) {\n    switch (p) {\n";
     for (int p = 0; p < npass; ++p) {
         const int r0 = r_lo + p * rt;
         const int rows = std::min(rt, r_hi - r0);

@@ -133,3 +133,18 @@ class MerkleTree:
 
     def into_values(self):
         return self._values
+
+
+SEND_STATS = {"trees": 0, "launches": 0}
+
+
+def send_shards_batch(items):
+    """Checker twin of hbbft_amd.send_shards_batch: orc.send_shards per item
+    (frame + encode + tree of broadcast.rs:170-204)."""
+    out = []
+    for n, value in items:
+        shards, nodes = orc.send_shards(n, (n - 1) // 3, bytes(value))
+        out.append(MerkleTree([shards[j].tobytes() for j in range(n)], nodes))
+    SEND_STATS["trees"] += len(items)
+    SEND_STATS["launches"] += 1
+    return out

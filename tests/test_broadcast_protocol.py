@@ -21,7 +21,7 @@ import pytest
 
 import virtual_net as vn
 from hbbft_amd.broadcast import (Broadcast, BroadcastError, ErrorKind, FaultKind, Message,
-                                 Target, ValidatorSet)
+                                 Target, ValidatorSet, broadcast_many)
 
 
 def _oracle_backend():
@@ -344,3 +344,79 @@ def test_lockstep_batched_validation(backend):
     assert launches > 0 and batched > launches      # several proofs per launch
     assert st["single"] - before["single"] < batched  # only adversary-injected proofs go alone
 
+
+
+def _epoch_value(n, p):
+    # ragged contributions: several proposers share a length (one batch), one
+    # is empty, the rest differ
+    return bytes((7 * p + i) & 0xFF for i in range(0 if p == 1 else 40 * (p % 3) + 3 * (p // 3 % 2)))
+
+
+def test_epoch_batched_inputs(backend):
+    """one epoch in which every validator proposes (Subset runs
+    N broadcasts, subset/proposal_state.rs:69-113), all proposers' framing,
+    encode and trees built by `broadcast_many` in a few batched launches;
+    every node's outputs, faults and crank counts equal the one-input-at-a-time
+    run of the same seeds."""
+    def make(n, p, seed):
+        rng = random.Random(seed)
+        ids = list(range(n))
+        net = vn.VirtualNet(ids, vn.max_faulty(n), lambda j: Broadcast(j, ids, p, backend=backend),
+                            vn.RandomAdversary(0.2, 0.2, backend), rng, message_limit=10_000 * n)
+        return net, _epoch_value(n, p), p
+
+    plan = [(n, p, 7000 + 100 * n + p) for n in (3, 4, 7) for p in range(n)]
+    seq = [make(*x) for x in plan]
+    for net, value, p in seq:
+        vn.run_broadcast(net, value, p)
+    st = backend.SEND_STATS
+    before = dict(st)
+    lock = [make(*x) for x in plan]
+    vn.run_lockstep(lock, backend, batched_input=True)
+    for (a, _, _), (b, _, _) in zip(seq, lock):
+        for na, nb in zip(a.nodes.values(), b.nodes.values()):
+            assert na.outputs == nb.outputs
+            assert [(f.node_id, f.kind) for f in na.faults] == [(f.node_id, f.kind) for f in nb.faults]
+        assert a.crank_count == b.crank_count
+    assert st["trees"] - before["trees"] == len(plan)
+    assert st["launches"] - before["launches"] < len(plan)
+
+
+def test_broadcast_many_errors(backend):
+    """`broadcast_many` keeps `broadcast`'s per-instance errors
+    (broadcast.rs:123-137): a non-proposer raises InstanceCannotPropose, a
+    second input MultipleInputs."""
+    ids = list(range(4))
+    prop = Broadcast(0, ids, 0, backend=backend)
+    other = Broadcast(1, ids, 0, backend=backend)
+    with pytest.raises(BroadcastError) as e:
+        broadcast_many([(other, b"x")], backend)
+    assert e.value.kind == ErrorKind.InstanceCannotPropose
+    steps = broadcast_many([(prop, b"abc")], backend)
+    fresh = Broadcast(0, ids, 0, backend=backend).broadcast(b"abc")
+    assert [(repr(t.target), t.message) for t in steps[0].messages] == \
+        [(repr(t.target), t.message) for t in fresh.messages]   # 3 Values, Echo, EchoHash
+    with pytest.raises(BroadcastError) as e:
+        broadcast_many([(prop, b"abc")], backend)
+    assert e.value.kind == ErrorKind.MultipleInputs
+
+
+@pytest.mark.gpu
+def test_send_shards_batch_matches_oracle():
+    """hbbft_amd.send_shards_batch (batched frame+encode+tree on the MI355X)
+    against the oracle's send_shards for ragged payloads at N = 1..64: every
+    shard, every tree node and every proof bit-exact."""
+    hb = _hip_backend()
+    orb = _oracle_backend()
+    items = [(n, bytes((13 * n + 5 * i + j) & 0xFF for j in range(L)))
+             for n in (1, 2, 3, 4, 7, 16, 64) for i, L in enumerate((0, 1, 5, 5, 100, 1000, 4099, 1000))]
+    got = hb.send_shards_batch(items)
+    want = orb.send_shards_batch(items)
+    for (n, _), g, w in zip(items, got, want):
+        assert g.values() == w.values()
+        assert g.root_hash() == w.root_hash()
+        for i in range(n):
+            pg, pw = g.proof(i), w.proof(i)
+            assert (pg.value(), pg.index(), pg.digests(), pg.root_hash()) == \
+                (pw.value(), pw.index(), pw.digests(), pw.root_hash())
+        assert g.proof(n) is None

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from hbbft_amd.broadcast import Broadcast, Message, prevalidate  # noqa: E402
+from hbbft_amd.broadcast import Broadcast, Message, broadcast_many, prevalidate  # noqa: E402
 
 
 class CrankError(AssertionError):
@@ -254,16 +254,23 @@ def check_outcome(net, value, proposer_id):
     return net
 
 
-def run_lockstep(items, backend):
+def run_lockstep(items, backend, batched_input=False):
     """Many broadcast networks cranked in lockstep, one crank per network per
     round.  Before every round the Value / Echo proofs all networks queued
     since the previous round are validated together, one batched launch per
     tree size (hbbft_amd.broadcast.prevalidate); the state machines then find
     every result memoised.  Each network's schedule depends only on its own
     RNG and state, so outcomes equal those of `run_broadcast`.
-    items: [(net, value, proposer)]."""
-    for net, value, proposer in items:
-        net.send_input(proposer, value)
+    batched_input: the proposers' inputs go through `broadcast_many` (one
+    frame+encode+tree launch per size) instead of one
+    `send_input` each.  items: [(net, value, proposer)]."""
+    if batched_input:
+        steps = broadcast_many([(net.nodes[p].algo, v) for net, v, p in items], backend)
+        for (net, _, proposer), step in zip(items, steps):
+            net.process_step(proposer, step)
+    else:
+        for net, value, proposer in items:
+            net.send_input(proposer, value)
     live = list(items)
     while live:
         by_n = {}
