@@ -69,7 +69,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if os.environ.get("HBRBC_BENCH_REHEARSE") == "1":
+        # multi-rank rehearsal on a box with fewer GPUs than ranks: gloo, ranks
+        # share the visible devices (the real N > 1 runs use RCCL, one GPU each)
+        local = local % torch.cuda.device_count()
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
