@@ -354,7 +354,9 @@ std::string jit_dir() {
 }
 
 std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth, int r_lo) {
-    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) + "_v9.co";
+    const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
+    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) +
+           (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) + "_v10.co";
 }
 
 // Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).
