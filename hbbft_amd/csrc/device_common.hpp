@@ -115,6 +115,9 @@ __device__ __forceinline__ void keccak_f1600(uint32_t (&L)[25], uint32_t (&H)[25
     }
 }
 
+#ifndef HB_SPONGE_V16
+#define HB_SPONGE_V16 1
+#endif
 // SHA3-256 of `len` bytes at `p` (8-byte aligned; the 8-byte word holding
 // the last byte must be readable).  Per-lane pointer and length; when every
 // lane of a wave has the same length all branches are wave-uniform.
@@ -125,6 +128,73 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     for (int i = 0; i < 25; ++i) L[i] = H[i] = 0u;
     const uint2 *q = reinterpret_cast<const uint2 *>(p);
     const uint32_t nfull = len / 136u;
+#if HB_SPONGE_V16
+    // 16-byte-aligned rows (every slab row): block t starts 8*t mod 16 bytes
+    // past a 16-byte boundary, so an even block is eight 16-byte loads and
+    // one 8-byte load and an odd block one 8-byte load and eight 16-byte
+    // loads -- 9 memory instructions per block instead of 17.  Blocks go in
+    // pairs, software-pipelined like the 8-byte path below.  Taken only when
+    // the grid holds fewer than 4 waves per SIMD (2^18 lanes): there it hides
+    // memory latency (cfg2, 65536 rows: leaf hash 23.6 -> 22.8 ms); at full
+    // occupancy (cfg3, 1 M rows) it measured 1 % slower than 8-byte loads.
+    const bool low_occ = (uint64_t)gridDim.x * blockDim.x < (1u << 18);
+    if (nfull >= 2 && low_occ && (reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+        uint4 e[8], o[8];
+        uint2 e8, o0;
+        auto load_even = [&](const uint2 *b) {
+            const uint4 *b4 = reinterpret_cast<const uint4 *>(b);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) e[i] = b4[i];
+            e8 = b[16];
+        };
+        auto load_odd = [&](const uint2 *b) {
+            o0 = b[0];
+            const uint4 *b4 = reinterpret_cast<const uint4 *>(b + 1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = b4[i];
+        };
+        load_even(q);
+        uint32_t t = 0;
+        for (; t + 2 <= nfull; t += 2) {
+            load_odd(q + 17);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                L[2 * i] ^= e[i].x;
+                H[2 * i] ^= e[i].y;
+                L[2 * i + 1] ^= e[i].z;
+                H[2 * i + 1] ^= e[i].w;
+            }
+            L[16] ^= e8.x;
+            H[16] ^= e8.y;
+            keccak_f1600(L, H);
+            q += 34;
+            if (t + 3 <= nfull) load_even(q);
+            L[0] ^= o0.x;
+            H[0] ^= o0.y;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                L[2 * i + 1] ^= o[i].x;
+                H[2 * i + 1] ^= o[i].y;
+                L[2 * i + 2] ^= o[i].z;
+                H[2 * i + 2] ^= o[i].w;
+            }
+            keccak_f1600(L, H);
+        }
+        if (t < nfull) {   // one even block left, already loaded
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                L[2 * i] ^= e[i].x;
+                H[2 * i] ^= e[i].y;
+                L[2 * i + 1] ^= e[i].z;
+                H[2 * i + 1] ^= e[i].w;
+            }
+            L[16] ^= e8.x;
+            H[16] ^= e8.y;
+            keccak_f1600(L, H);
+            q += 17;
+        }
+    } else
+#endif
     // Full blocks, software-pipelined: block t+1 is loaded while block t is
     // permuted, so the sponge never waits on memory between permutations
     // (+34 VGPRs; the sponge kernels run at 4 waves/SIMD either way).
