@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(
 // inv(M[valid]) (missing data rows are rows of the inverse; missing parity
 // rows equal rse's parity-from-rebuilt-data by linearity over GF(2^8)),
 // expanded to split-2-bit tables for gf_apply_kernel.
-__global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
+__global__ __launch_bounds__(256) void decode_matrix_kernel(
     int n, int k, int rt, int raw, const uint8_t *__restrict__ matrix,
     const uint8_t *__restrict__ present, uint4 *__restrict__ tables,
     uint32_t *__restrict__ in_idx, uint32_t *__restrict__ out_idx, int *__restrict__ nout,
@@ -518,10 +518,11 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
     const int m = n - k;
     const size_t inst = blockIdx.x;
     const int tid = threadIdx.x;
+    const int nt = (int)blockDim.x;  // one wave (k <= 64) or four
     const uint8_t *pres = present + inst * (size_t)n;
 
-    for (int i = tid; i < 512; i += kBlock) exp_t[i] = kGf.exp[i];
-    for (int i = tid; i < 256; i += kBlock) log_t[i] = kGf.log[i];
+    for (int i = tid; i < 512; i += nt) exp_t[i] = kGf.exp[i];
+    for (int i = tid; i < 256; i += nt) log_t[i] = kGf.log[i];
     if (tid == 0) {
         int np = 0, nm = 0, nv = 0;
         for (int i = 0; i < n; ++i) {
@@ -546,20 +547,23 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
         return;
     }
     const int w2 = 2 * k;
-    for (int e = tid; e < k * w2; e += kBlock) {
+    for (int e = tid; e < k * w2; e += nt) {
         const int r = e / w2, c = e - r * w2;
         aug[e] = (c < k) ? matrix[(size_t)valid[r] * k + c] : (uint8_t)((c - k) == r);
     }
     __syncthreads();
     for (int c = 0; c < k; ++c) {
-        if (tid == 0) {
+        if (tid < 64) {   // pivot: first nonzero row at or below c, by ballot over 64 rows
             int p = -1;
-            for (int r = c; r < k; ++r)
-                if (aug[r * w2 + c]) {
-                    p = r;
-                    break;
-                }
-            meta[2] = p;
+            for (int r0 = c; r0 < k && p < 0; r0 += 64) {
+                const int r = r0 + tid;
+                const unsigned long long bal = __ballot(r < k && aug[r * w2 + c] != 0);
+                if (bal) p = r0 + __ffsll((long long)bal) - 1;
+            }
+            if (tid == 0) meta[2] = p;
+        }
+        if (tid == 0) {
+            const int p = meta[2];
             if (p < 0)
                 meta[4] = 1;
             else
@@ -576,19 +580,19 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
         const int p = meta[2];
         const uint8_t inv = (uint8_t)meta[3];
         if (p != c) {
-            for (int col = tid; col < w2; col += kBlock) {
+            for (int col = tid; col < w2; col += nt) {
                 uint8_t t = aug[c * w2 + col];
                 aug[c * w2 + col] = aug[p * w2 + col];
                 aug[p * w2 + col] = t;
             }
         }
         __syncthreads();
-        for (int col = tid; col < w2; col += kBlock)
+        for (int col = tid; col < w2; col += nt)
             aug[c * w2 + col] = gf_mul_lds(exp_t, log_t, inv, aug[c * w2 + col]);
         __syncthreads();
-        for (int r = tid; r < k; r += kBlock) fac[r] = (r == c) ? 0 : aug[r * w2 + c];
+        for (int r = tid; r < k; r += nt) fac[r] = (r == c) ? 0 : aug[r * w2 + c];
         __syncthreads();
-        for (int e = tid; e < k * w2; e += kBlock) {
+        for (int e = tid; e < k * w2; e += nt) {
             const int r = e / w2, col = e - r * w2;
             const uint8_t f = fac[r];
             if (f) aug[e] ^= gf_mul_lds(exp_t, log_t, f, aug[c * w2 + col]);
@@ -598,7 +602,7 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
     const int npass = (m + rt - 1) / rt;
     uint4 *tab = tables + inst * (size_t)npass * rt * k;
     const int nrows = (nm + rt - 1) / rt * rt;  // pad the last pass with zero rows
-    for (int e = tid; e < nrows * k; e += kBlock) {
+    for (int e = tid; e < nrows * k; e += nt) {
         const int t = e / k, c = e - t * k;
         const int row = t < nm ? missing[t] : -1;
         uint8_t coef;
@@ -616,8 +620,8 @@ __global__ __launch_bounds__(kBlock) void decode_matrix_kernel(
         else      // perm kernel: split-2-bit entries [pass][j][rt]
             tab[((size_t)(t / rt) * k + c) * rt + (t % rt)] = gf_split2_entry(coef, exp_t, log_t);
     }
-    for (int j = tid; j < k; j += kBlock) in_idx[inst * (size_t)k + j] = valid[j];
-    for (int t = tid; t < nm; t += kBlock) out_idx[inst * (size_t)m + t] = missing[t];
+    for (int j = tid; j < k; j += nt) in_idx[inst * (size_t)k + j] = valid[j];
+    for (int t = tid; t < nm; t += nt) out_idx[inst * (size_t)m + t] = missing[t];
     if (tid == 0) {
         nout[inst] = nm;
         status[inst] = 0;
@@ -932,7 +936,16 @@ hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
 hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
-    hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(kBlock), lds, s, a.n,
+    // one wave per instance for small systems: no cross-wave barriers, more
+    // instances per CU (k = 22: 0.46 -> 0.34 ms per 16384 instances); at
+    // k = 44 one wave has too many elements per column (1.05 -> 1.42 ms), so
+    // larger systems keep four waves.  HBRBC_DM_THREADS=64|256 forces either.
+    static const int force = [] {
+        const char *e = getenv("HBRBC_DM_THREADS");
+        return e ? atoi(e) : 0;
+    }();
+    const int threads = force == 64 || force == 256 ? force : (a.k <= 32 ? 64 : kBlock);
+    hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(threads), lds, s, a.n,
                        a.k, a.rt, a.raw, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
     return hipGetLastError();
 }
