@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(
 // inv(M[valid]) (missing data rows are rows of the inverse; missing parity
 // rows equal rse's parity-from-rebuilt-data by linearity over GF(2^8)),
 // expanded to split-2-bit tables for gf_apply_kernel.
-__global__ __launch_bounds__(256) void decode_matrix_kernel(
+__global__ __launch_bounds__(1024) void decode_matrix_kernel(
     int n, int k, int rt, int raw, const uint8_t *__restrict__ matrix,
     const uint8_t *__restrict__ present, uint4 *__restrict__ tables,
     uint32_t *__restrict__ in_idx, uint32_t *__restrict__ out_idx, int *__restrict__ nout,
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void decode_matrix_kernel(
     const int m = n - k;
     const size_t inst = blockIdx.x;
     const int tid = threadIdx.x;
-    const int nt = (int)blockDim.x;  // one wave (k <= 64) or four
+    const int nt = (int)blockDim.x;  // 64, 256 or 512 threads by k (launch_decode_matrix)
     const uint8_t *pres = present + inst * (size_t)n;
 
     for (int i = tid; i < 512; i += nt) exp_t[i] = kGf.exp[i];
@@ -936,15 +936,17 @@ hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
 hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
-    // one wave per instance for small systems: no cross-wave barriers, more
-    // instances per CU (k = 22: 0.46 -> 0.34 ms per 16384 instances); at
-    // k = 44 one wave has too many elements per column (1.05 -> 1.42 ms), so
-    // larger systems keep four waves.  HBRBC_DM_THREADS=64|256 forces either.
+    // threads per instance by system size (measured per step): k = 22 one
+    // wave, 0.46 -> 0.34 ms (no cross-wave barriers, more instances per CU);
+    // k = 44 four waves (one: 1.42, two: 1.08, four: 1.04, eight: 1.22 ms);
+    // k = 84 eight waves (four: 1.60, eight: 1.19, sixteen: 1.23 ms).
+    // HBRBC_DM_THREADS=64..1024 forces a size.
     static const int force = [] {
         const char *e = getenv("HBRBC_DM_THREADS");
         return e ? atoi(e) : 0;
     }();
-    const int threads = force == 64 || force == 256 ? force : (a.k <= 32 ? 64 : kBlock);
+    const int threads = (force >= 64 && force <= 1024 && force % 64 == 0) ? force
+                                                                         : (a.k <= 32 ? 64 : a.k <= 64 ? 256 : 512);
     hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(threads), lds, s, a.n,
                        a.k, a.rt, a.raw, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
     return hipGetLastError();
