@@ -17,7 +17,8 @@ __all__ = [
     "RseError", "HbrbcUnavailable", "Coding", "MerkleTree", "Proof", "RbcBatch",
     "shard_len", "merkle_node_count", "max_proof_len", "lib", "LIB_PATH", "STAGES",
     "jit_build_encode", "jit_file_name", "WIRE_VARIANTS", "validate_proofs", "VALIDATE_STATS",
-    "send_shards_batch", "SEND_STATS",
+    "send_shards_batch", "SEND_STATS", "jit_decode_groups", "jit_build_decode",
+    "jit_decode_file_name", "jit_encode_groups",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -106,6 +107,21 @@ def lib():
         "hbrbc_jit_encode_groups": (_S, [_S, _S]),
         "hbrbc_jit_build_encode_group": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p]),
         "hbrbc_jit_file_name": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p, _S]),
+        "hbrbc_frame_encode_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _S, _S, _S, _S, _P]),
+        "hbrbc_merkle_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _S, _S, _P, _S, _P]),
+        "hbrbc_validate_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _S, _S, _P, _P, _P, _P, _S,
+                                               _P, _S, _S, _S, _P, _P, _S, _P]),
+        "hbrbc_reconstruct_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _S, _P, _S, _P, _P]),
+        "hbrbc_decode_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _S, _P, _S, _P, _S, _P, _S,
+                                             ctypes.c_int, _P, _S, _P, _P, _P]),
+        "hbrbc_decode_cache_clear": (ctypes.c_int, [_P]),
+        "hbrbc_decode_cache_fill": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint32)]),
+        "hbrbc_decoder_specialise": (ctypes.c_int, [_P, _P, _S]),
+        "hbrbc_jit_build_encode_rows": (ctypes.c_int, [_S, _S, _S, _S, ctypes.c_char_p]),
+        "hbrbc_jit_encode_file_name": (ctypes.c_int, [_S, _S, _S, _S, ctypes.c_char_p, _S]),
+        "hbrbc_jit_decode_groups": (_S, [_S, _S, _P]),
+        "hbrbc_jit_build_decode": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p]),
+        "hbrbc_jit_decode_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p, _S]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -122,21 +138,51 @@ def _check(code):
         raise RseError(code, lib().hbrbc_last_error().decode(errors="replace"))
 
 
-def jit_build_encode(data_shards, parity_shards, directory=None, group=None):
+def jit_build_encode(data_shards, parity_shards, directory=None, group=None, rows_per_block=0):
     """Generate + compile (hiprtc, gfx950; no GPU needed) the specialised RS
     encoder for this matrix into the code-object cache (jit.hip): every
-    parity-row group, or just `group`."""
+    parity-row group, or just `group`; rows_per_block < n builds the variant
+    for that blocked row layout."""
     d = directory.encode() if directory else None
-    if group is None:
-        _check(lib().hbrbc_jit_build_encode(data_shards, parity_shards, d))
-    else:
-        _check(lib().hbrbc_jit_build_encode_group(data_shards, parity_shards, group, d))
+    groups = range(jit_encode_groups(data_shards, parity_shards)) if group is None else [group]
+    for g in groups:
+        _check(lib().hbrbc_jit_build_encode_rows(data_shards, parity_shards, g, rows_per_block, d))
 
 
-def jit_file_name(data_shards, parity_shards, group=0):
+def jit_file_name(data_shards, parity_shards, group=0, rows_per_block=0):
     """Cache file name of one group's specialised-encoder code object."""
     buf = ctypes.create_string_buffer(256)
-    _check(lib().hbrbc_jit_file_name(data_shards, parity_shards, group, buf, 256))
+    _check(lib().hbrbc_jit_encode_file_name(data_shards, parity_shards, group, rows_per_block,
+                                            buf, 256))
+    return buf.value.decode()
+
+
+def _mask_buffer(present):
+    import numpy as np
+    return np.ascontiguousarray(np.asarray(present, dtype=np.uint8) != 0, dtype=np.uint8)
+
+
+def jit_decode_groups(data_shards, parity_shards, present):
+    """Code objects (output-row groups) of the decoder specialised for an
+    erasure pattern (present: n flags)."""
+    m = _mask_buffer(present)
+    return lib().hbrbc_jit_decode_groups(data_shards, parity_shards, m.ctypes.data)
+
+
+def jit_build_decode(data_shards, parity_shards, present, group, rows_per_block=0,
+                     directory=None):
+    """Compile one group of the pattern-specialised decoder into the cache."""
+    m = _mask_buffer(present)
+    d = directory.encode() if directory else None
+    _check(lib().hbrbc_jit_build_decode(data_shards, parity_shards, m.ctypes.data,
+                                        rows_per_block, group, d))
+
+
+def jit_decode_file_name(data_shards, parity_shards, present, group=0, rows_per_block=0):
+    m = _mask_buffer(present)
+    buf = ctypes.create_string_buffer(256)
+    _check(lib().hbrbc_jit_decode_file_name(data_shards, parity_shards, m.ctypes.data,
+                                            rows_per_block, group, buf, 256))
     return buf.value.decode()
 
 
@@ -218,7 +264,7 @@ class Coding:
         return lib().hbrbc_data_shard_count(self._h)
 
     def encode_kernel(self):
-        """Which encode kernel this context runs: specialised / bitslice / perm / trivial."""
+        """Which encode kernel this context runs: specialised / bitslice / trivial."""
         return lib().hbrbc_encode_kernel(self._h).decode()
 
     def parity_shard_count(self):
@@ -536,6 +582,59 @@ class RbcBatch:
                                           values.stride(0), per_inst, _ptr(indices), _ptr(digests),
                                           _ptr(ndig), _ptr(roots), roots.stride(0), self.n, count,
                                           _ptr(ok), self._stream(stream)))
+
+    # -- blocked row layouts (hbrbc.h "*_rows"): row j of instance i at
+    #    base + i*inst_stride + (j // rpb)*block_stride + (j % rpb)*shard_stride
+    def frame_encode_rows(self, payloads, plen, base, count, shard_stride, rows_per_block,
+                          block_stride, inst_stride, stream=None):
+        S = shard_len(plen, self.k)
+        _check(lib().hbrbc_frame_encode_rows(self.coding.handle, _ptr(payloads), payloads.stride(0),
+                                             plen, count, _ptr(base), S, shard_stride,
+                                             rows_per_block, block_stride, inst_stride,
+                                             self._stream(stream)))
+
+    def merkle_rows(self, base, S, count, shard_stride, rows_per_block, block_stride, inst_stride,
+                    nodes, stream=None):
+        _check(lib().hbrbc_merkle_rows(self.coding.handle, _ptr(base), S, shard_stride,
+                                       rows_per_block, block_stride, inst_stride, count,
+                                       _ptr(nodes), nodes.stride(0), self._stream(stream)))
+
+    def validate_layout(self, base, S, count, per_inst, shard_stride, rows_per_block, block_stride,
+                        inst_stride, digests, ndig, digest_rows, roots, ok, rows=None,
+                        indices=None, leaf_out=None, stream=None):
+        """Proof::validate of `per_inst` rows (`rows`: int32 device list, or
+        0..per_inst-1) of every instance in a (blocked) row layout; digests
+        [count, digest_rows, dslots, 32], ndig [count, digest_rows]; leaf_out:
+        node slab [count, node_count, 32] whose level 0 receives the leaves."""
+        _check(lib().hbrbc_validate_rows(
+            self.coding.handle, _ptr(base), S, shard_stride, rows_per_block, block_stride,
+            inst_stride, per_inst, _ptr(rows), _ptr(indices), _ptr(digests), _ptr(ndig),
+            digest_rows, _ptr(roots), roots.stride(0), self.n, count, _ptr(ok), _ptr(leaf_out),
+            leaf_out.stride(0) if leaf_out is not None else 0, self._stream(stream)))
+
+    def decode_rows(self, base, S, count, shard_stride, rows_per_block, block_stride, inst_stride,
+                    present, roots, nodes, payload_out, plen_out, status, known_leaves=False,
+                    stream=None):
+        _check(lib().hbrbc_decode_rows(
+            self.coding.handle, _ptr(base), S, shard_stride, rows_per_block, block_stride,
+            inst_stride, _ptr(present), count, _ptr(roots), roots.stride(0), _ptr(nodes),
+            nodes.stride(0), 1 if known_leaves else 0, _ptr(payload_out), payload_out.stride(0),
+            _ptr(plen_out), _ptr(status), self._stream(stream)))
+
+    def specialise_decoder(self, present, rows_per_block=0):
+        """hbrbc_decoder_specialise: an XOR-network decoder for one erasure
+        pattern (present: n flags) in layouts with this rows_per_block."""
+        m = _mask_buffer(present)
+        assert m.size == self.n
+        _check(lib().hbrbc_decoder_specialise(self.coding.handle, m.ctypes.data, rows_per_block))
+
+    def decode_cache_clear(self):
+        _check(lib().hbrbc_decode_cache_clear(self.coding.handle))
+
+    def decode_cache_fill(self):
+        v = ctypes.c_uint32(0)
+        _check(lib().hbrbc_decode_cache_fill(self.coding.handle, ctypes.byref(v)))
+        return v.value
 
     def reconstruct(self, slab, S, present, status, stream=None):
         _check(lib().hbrbc_reconstruct_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),

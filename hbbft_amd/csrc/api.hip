@@ -2,16 +2,18 @@
 //
 // Host-side responsibilities only: argument checks with the reference's
 // error semantics, the encoding matrix (rse `build_matrix`, computed once per
-// context exactly like `ReedSolomon::new`), device workspaces, and launch
+// context exactly like `ReedSolomon::new`), device workspaces (the
+// decode-matrix cache among them), specialised-kernel modules, and launch
 // sequencing.  Every byte of shard, digest and payload data is computed by
-// the HIP kernels in kernels.hip; there is no CPU fallback.
+// the HIP kernels in kernels.hip / jit.hip; there is no CPU fallback.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
-#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -127,6 +129,44 @@ bool build_matrix(size_t k, size_t total, std::vector<uint8_t> &out) {
     return true;
 }
 
+// The recovery rows of one erasure pattern, as rse reconstruct would use
+// them: valid = the first k present rows, missing = every absent row;
+// rows[t] = M[missing[t]] * inv(M[valid]) (a missing data row is a row of the
+// inverse).  false: fewer than k present, none missing or a singular block.
+bool recovery_rows(const std::vector<uint8_t> &mat, size_t k, size_t n, const uint8_t *present,
+                   std::vector<int> &valid, std::vector<int> &missing,
+                   std::vector<uint8_t> &rows) {
+    const HostGf &g = gf();
+    valid.clear();
+    missing.clear();
+    for (size_t i = 0; i < n; ++i) {
+        if (present[i]) {
+            if (valid.size() < k) valid.push_back((int)i);
+        } else {
+            missing.push_back((int)i);
+        }
+    }
+    if (valid.size() < k || missing.empty()) return false;
+    std::vector<uint8_t> sub(k * k);
+    for (size_t r = 0; r < k; ++r)
+        for (size_t c = 0; c < k; ++c) sub[r * k + c] = mat[(size_t)valid[r] * k + c];
+    if (!gf_invert(k, sub)) return false;
+    rows.assign(missing.size() * k, 0);
+    for (size_t t = 0; t < missing.size(); ++t) {
+        const size_t row = (size_t)missing[t];
+        for (size_t c = 0; c < k; ++c) {
+            uint8_t acc = 0;
+            if (row < k) {
+                acc = sub[row * k + c];
+            } else {
+                for (size_t j = 0; j < k; ++j) acc ^= g.mul(mat[row * k + j], sub[j * k + c]);
+            }
+            rows[t * k + c] = acc;
+        }
+    }
+    return true;
+}
+
 // Grow-only device buffer.
 struct DevBuf {
     void *p = nullptr;
@@ -155,33 +195,84 @@ struct DevBuf {
     }
 };
 
+// Grow-only pinned host buffer (staging of the per-call shims: one DMA per
+// direction instead of one pageable copy per shard).
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t b = round_up(bytes < 4096 ? 4096 : bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, b, hipHostMallocDefault);
+        if (e == hipSuccess) cap = b;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+// rows_per_block (ABI) -> RowMap / code-object block size
+RowMap make_rows(size_t n, size_t shard_stride, size_t rows_per_block, size_t block_stride) {
+    RowMap r = plain_rows(shard_stride);
+    if (rows_per_block && rows_per_block < n) {
+        r.rb = (uint32_t)rows_per_block;
+        r.bst = block_stride;
+    }
+    return r;
+}
+inline int code_rb(const RowMap &r) { return r.plain() ? 256 : (int)r.rb; }
+
 }  // namespace
 
 struct hbrbc_ctx {
     int device = 0;
     size_t k = 0, m = 0, n = 0;
     int rt_enc = 2, rt_rec = 2;  // GF row tiles (rows per pass) for encode / reconstruct
-    int bitslice = 1;            // GF kernel: 1 bit-sliced (default), 0 split-2-bit v_perm
+    int gf_mode = 0;             // generic kernel: 0 branch per bit, 1 hinted, 2 masked
     std::vector<uint8_t> matrix;  // n x k
     hipStream_t stream = nullptr;
-    // specialised encoder (jit.hip) for this matrix, when its code object is available
-    // specialised encoder (jit.hip), one module per parity-row group
+    // specialised XOR-network modules (jit.hip): one module per output-row group
     struct SpecGroup {
         int r_lo, r_hi;
         hipModule_t mod;
-        hipFunction_t enc, fe;       // encode / frame+encode twin
+        hipFunction_t fn, fe;        // kernel / frame+encode twin (encoder only)
     };
-    std::vector<SpecGroup> spec;
-    int rt_spec = 2;              // parity rows per pass of the specialised encoder
-    int depth_spec = 4;           // its data-row prefetch depth
+    // encoder modules by code-object row block (256 = plain layout); an
+    // empty vector records a failed load
+    std::map<int, std::vector<SpecGroup>> enc_spec;
+    int rt_spec = 2;              // output rows per pass of the specialised kernels
+    int depth_spec = 4;           // their input-row prefetch depth
     std::string enc_kind = "none";
-    DevBuf d_matrix, d_enc_tables, d_enc_in, d_enc_out;
-    // reconstruct workspace
+    // pattern-specialised decoders: at most one per code-object row block
+    struct DecSpec {
+        uint64_t hash;
+        int rt;
+        std::vector<SpecGroup> groups;
+    };
+    std::map<int, DecSpec> dec_spec;
+    DevBuf d_matrix, d_enc_coefs, d_enc_in, d_enc_out;
+    // reconstruct workspace: decode-matrix cache + per-call scratch
     size_t ws_count = 0;
-    DevBuf ws_tables, ws_in, ws_out, ws_nout, ws_status, ws_plen;
+    int pc_cap = 0;
+    size_t pc_inserted = 0;       // upper bound of shared slots filled since the last clear
+    DevBuf pc_hash, pc_keys, pc_coefs, pc_in, pc_out, pc_nout, pc_status, pc_fill;
+    DevBuf ws_pat, ws_own, ws_status, ws_list, ws_counter;
     // per-call shim staging
     std::mutex shim_mu;
-    DevBuf st_slab, st_present, st_status, st_nodes, st_aux, st_aux2, st_aux3;
+    DevBuf st_slab, st_nodes, st_aux;
+    PinBuf pin;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -200,6 +291,7 @@ struct hbrbc_ctx {
         }
         return ev_pool[ev_used++];
     }
+    size_t coef_stride() const { return (m + rt_rec - 1) / rt_rec * k * 16 + 16; }
 };
 
 namespace {
@@ -232,7 +324,7 @@ struct StageTimer {
 inline hipStream_t pick(hbrbc_ctx *, void *stream) { return static_cast<hipStream_t>(stream); }
 
 int check_slab(const void *base, size_t shard_len, size_t shard_stride, size_t inst_stride,
-               size_t n, size_t count) {
+               size_t n, size_t count, size_t rows_per_block = 0, size_t block_stride = 0) {
     if (count == 0) return HBRBC_OK;
     if (!base) return fail(HBRBC_E_INVALID_ARG, "null shard slab");
     if (reinterpret_cast<uintptr_t>(base) % 16)
@@ -240,10 +332,24 @@ int check_slab(const void *base, size_t shard_len, size_t shard_stride, size_t i
     if (shard_stride % 16 || shard_stride < shard_len)
         return fail(HBRBC_E_INVALID_ARG, "shard_stride %zu must be a multiple of 16 and >= %zu",
                     shard_stride, shard_len);
+    if (shard_len > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "shard_len too large");
+    if (rows_per_block && rows_per_block < n) {
+        // blocked rows: blocks of rows_per_block rows, instances interleaved inside a block
+        if (rows_per_block > 255)
+            return fail(HBRBC_E_INVALID_ARG, "rows_per_block %zu > 255", rows_per_block);
+        if (block_stride % 16 || inst_stride % 16 || inst_stride < rows_per_block * shard_stride)
+            return fail(HBRBC_E_INVALID_ARG, "blocked layout: inst_stride %zu must be a multiple "
+                        "of 16 and >= rows_per_block * shard_stride", inst_stride);
+        if (block_stride < count * inst_stride)
+            return fail(HBRBC_E_INVALID_ARG, "blocked layout: block_stride %zu < count * "
+                        "inst_stride", block_stride);
+        if ((uint64_t)rows_per_block * shard_stride >= 0x7FFFFFFFull)
+            return fail(HBRBC_E_INVALID_ARG, "row block larger than 2 GiB");
+        return HBRBC_OK;
+    }
     if (count > 1 && (inst_stride % 16 || inst_stride < n * shard_stride))
         return fail(HBRBC_E_INVALID_ARG, "inst_stride %zu must be a multiple of 16 and >= %zu",
                     inst_stride, n * shard_stride);
-    if (shard_len > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "shard_len too large");
     return HBRBC_OK;
 }
 
@@ -257,31 +363,67 @@ int check_nodes(const void *nodes, size_t node_inst_stride, size_t n, size_t cou
     return HBRBC_OK;
 }
 
-size_t rec_tab_rows(const hbrbc_ctx *c) {
-    return (c->m + c->rt_rec - 1) / c->rt_rec * c->rt_rec;
-}
-
+// Reconstruct workspace for `count` instances: the pattern cache (cap shared
+// slots, count private ones) and per-call scratch.  Growing it drops the cache.
 int ensure_workspace(hbrbc_ctx *c, size_t count) {
     if (count <= c->ws_count) return HBRBC_OK;
     const size_t k = c->k, m = c->m;
-    HB_HIP(c->ws_tables.ensure(count * rec_tab_rows(c) * k * sizeof(uint4) + 16));
-    HB_HIP(c->ws_in.ensure((count * k + 4) * sizeof(uint32_t)));
-    HB_HIP(c->ws_out.ensure((count * m + 4) * sizeof(uint32_t)));
-    HB_HIP(c->ws_nout.ensure(count * sizeof(int)));
+    int cap = 1024;
+    while ((size_t)cap < 2 * count) cap *= 2;
+    const size_t slots = (size_t)cap + count;
+    HB_HIP(c->pc_hash.ensure((size_t)cap * sizeof(uint64_t)));
+    HB_HIP(c->pc_keys.ensure(slots * 8 * sizeof(uint32_t)));
+    HB_HIP(c->pc_coefs.ensure(slots * c->coef_stride()));
+    HB_HIP(c->pc_in.ensure((slots * k + 4) * sizeof(uint32_t)));
+    HB_HIP(c->pc_out.ensure((slots * m + 4) * sizeof(uint32_t)));
+    HB_HIP(c->pc_nout.ensure(slots * sizeof(int)));
+    HB_HIP(c->pc_status.ensure(slots * sizeof(int32_t)));
+    HB_HIP(c->pc_fill.ensure(sizeof(uint32_t)));
+    HB_HIP(c->ws_pat.ensure(count * sizeof(int)));
+    HB_HIP(c->ws_own.ensure(count));
     HB_HIP(c->ws_status.ensure(count * sizeof(int32_t)));
-    HB_HIP(c->ws_plen.ensure(count * sizeof(uint32_t)));
+    HB_HIP(c->ws_list.ensure((count * std::max<size_t>(m, 1) + 1) * sizeof(uint2)));
+    HB_HIP(c->ws_counter.ensure(sizeof(uint32_t)));
+    HB_HIP(hipMemset(c->pc_hash.p, 0, (size_t)cap * sizeof(uint64_t)));
+    HB_HIP(hipMemset(c->pc_fill.p, 0, sizeof(uint32_t)));
+    c->pc_cap = cap;
+    c->pc_inserted = 0;
     c->ws_count = count;
     return HBRBC_OK;
 }
 
-// Leaf hashes + all levels into a node slab.
-int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, size_t shard_stride,
+PatternCache cache_view(hbrbc_ctx *c) {
+    PatternCache pc;
+    pc.hash = c->pc_hash.as<uint64_t>();
+    pc.keys = c->pc_keys.as<uint32_t>();
+    pc.coefs = c->pc_coefs.as<uint8_t>();
+    pc.coef_stride = c->coef_stride();
+    pc.in_idx = c->pc_in.as<uint32_t>();
+    pc.out_idx = c->pc_out.as<uint32_t>();
+    pc.nout = c->pc_nout.as<int>();
+    pc.status = c->pc_status.as<int32_t>();
+    pc.fill = c->pc_fill.as<uint32_t>();
+    pc.cap = c->pc_cap;
+    return pc;
+}
+
+// Leaf hashes + all levels into a node slab (known_leaves: level 0 holds the
+// leaves of every row but the ones the last reconstruct rebuilt).
+int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, const RowMap &rows,
                size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
-               size_t node_inst_stride, hipStream_t s) {
+               size_t node_inst_stride, bool known_leaves, hipStream_t s) {
     {
         StageTimer t(c, HBRBC_STAGE_LEAF_HASH, s);
-        HB_HIP(launch_leaf_hash(shards, shard_len, shard_stride, inst_stride, n, count, nodes,
-                                node_inst_stride, s));
+        if (!known_leaves) {
+            HB_HIP(launch_leaf_hash(shards, shard_len, rows, inst_stride, n, count, nodes,
+                                    node_inst_stride, s));
+        } else if (c->m > 0) {
+            HB_HIP(launch_leaf_hash_rebuilt(shards, shard_len, rows, inst_stride, count,
+                                            c->ws_pat.as<int>(), c->pc_out.as<uint32_t>(), c->m,
+                                            c->pc_nout.as<int>(), (int)c->m, nodes,
+                                            node_inst_stride, c->ws_counter.as<uint32_t>(),
+                                            c->ws_list.as<uint2>(), s));
+        }
     }
     StageTimer t(c, HBRBC_STAGE_TREE_LEVELS, s);
     size_t off = 0, sz = n;
@@ -294,53 +436,83 @@ int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, size_t sha
     return HBRBC_OK;
 }
 
-int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
+hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, XorArgs a,
+                            size_t count, hipStream_t s);
+
+int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &rows,
                     size_t inst_stride, const uint8_t *present, size_t count, int32_t *status,
                     hipStream_t s) {
     int st = ensure_workspace(c, count);
     if (st) return st;
+    // rse keeps an LRU of decode matrices; here the shared slots are flushed
+    // once the patterns inserted since the last flush could exceed 4x the
+    // table (a repeating pattern is then recomputed once per flush)
+    if (c->pc_inserted + count > 4 * (size_t)c->pc_cap) {
+        HB_HIP(hipMemsetAsync(c->pc_hash.p, 0, (size_t)c->pc_cap * sizeof(uint64_t), s));
+        HB_HIP(hipMemsetAsync(c->pc_fill.p, 0, sizeof(uint32_t), s));
+        c->pc_inserted = 0;
+    }
+    c->pc_inserted += count;
     {
         StageTimer t(c, HBRBC_STAGE_DECODE_MATRIX, s);
         DecodeMatrixArgs a;
         a.n = (int)c->n;
         a.k = (int)c->k;
         a.rt = c->rt_rec;
-        a.raw = c->bitslice;
         a.matrix = c->d_matrix.as<uint8_t>();
         a.present = present;
         a.count = count;
-        a.tables = c->ws_tables.as<uint4>();
-        a.in_idx = c->ws_in.as<uint32_t>();
-        a.out_idx = c->ws_out.as<uint32_t>();
-        a.nout = c->ws_nout.as<int>();
+        a.cache = cache_view(c);
+        a.pat = c->ws_pat.as<int>();
+        a.own = c->ws_own.as<uint8_t>();
         a.status = status;
         HB_HIP(launch_decode_matrix(a, s));
     }
     if (c->m == 0) return HBRBC_OK;  // Coding::Trivial: nothing to rebuild
     StageTimer t(c, HBRBC_STAGE_RECONSTRUCT, s);
-    GfApplyArgs g;
+    const auto ds = c->dec_spec.find(code_rb(rows));
+    const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
+    if (spec) {
+        XorArgs x{};
+        x.base = shards;
+        x.inst_stride = inst_stride;
+        x.shard_stride = rows.sst;
+        x.block_stride = rows.bst;
+        x.row_bytes = (unsigned)round_up(shard_len, 16);
+        x.pat = c->ws_pat.as<int>();
+        x.slot_hash = reinterpret_cast<const unsigned long *>(c->pc_hash.as<uint64_t>());
+        x.hash_slots = c->pc_cap;
+        x.p_only = -1;
+        for (const auto &g : ds->second.groups)
+            HB_HIP(launch_xor_group(g, false, ds->second.rt, x, count, s));
+    }
+    GfApplyArgs g{};
     g.base = shards;
     g.inst_stride = inst_stride;
-    g.shard_stride = shard_stride;
+    g.rows = rows;
     g.n16 = (int)((shard_len + 15) / 16);
-    g.tables = c->ws_tables.as<uint4>();
-    g.tab_inst_stride = rec_tab_rows(c) * c->k;
-    g.rt = c->rt_rec;
-    g.bitslice = c->bitslice;
-    g.in_idx = c->ws_in.as<uint32_t>();
+    g.coefs = c->pc_coefs.as<uint8_t>();
+    g.coef_slot_stride = c->coef_stride();
+    g.in_idx = c->pc_in.as<uint32_t>();
     g.in_idx_stride = c->k;
-    g.out_idx = c->ws_out.as<uint32_t>();
+    g.out_idx = c->pc_out.as<uint32_t>();
     g.out_idx_stride = c->m;
-    g.nout = c->ws_nout.as<int>();
+    g.nout = c->pc_nout.as<int>();
     g.nout_uniform = 0;
+    g.pat = c->ws_pat.as<int>();
+    g.slot_hash = c->pc_hash.as<uint64_t>();
+    g.skip_hash = spec ? ds->second.hash : 0;
+    g.hash_slots = c->pc_cap;
     g.max_rows = (int)c->m;
     g.nin = (int)c->k;
+    g.rt = c->rt_rec;
+    g.mode = c->gf_mode;
     g.count = count;
     HB_HIP(launch_gf_apply(g, s));
     return HBRBC_OK;
 }
 
-// Directory of cached specialised-encoder code objects: $HBRBC_JIT_DIR, else
+// Directory of cached specialised code objects: $HBRBC_JIT_DIR, else
 // <directory of libhbrbc.so>/jit.
 std::string jit_dir() {
     if (const char *e = getenv("HBRBC_JIT_DIR")) return e;
@@ -353,13 +525,13 @@ std::string jit_dir() {
     return "jit";
 }
 
-std::string jit_file(const std::string &dir, size_t k, size_t m, int rt, int depth, int r_lo) {
+std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
-    return dir + "/" + encode_kernel_name(k, m, rt, depth, false, r_lo) +
-           (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) + "_v10.co";
+    return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
+           "_v11.co";
 }
 
-// Data rows the specialised encoder keeps in flight (HBM latency at 2 waves/SIMD).
+// Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
 int spec_depth() {
     if (const char *e = getenv("HBRBC_JIT_DEPTH")) return std::max(1, std::min(8, atoi(e)));
     return 4;
@@ -377,99 +549,153 @@ bool read_file(const std::string &path, std::vector<char> &out) {
     return ok;
 }
 
-// Parity rows per pass of the specialised encoder: the accumulators (8 VGPRs
+bool write_file(const std::string &path, const std::vector<char> &code) {
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f) return false;
+    const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+    fclose(f);
+    return ok;
+}
+
+// Output rows per pass of the specialised kernels: the accumulators (8 VGPRs
 // per row) plus the planes, pair XORs and load buffers must stay near 200
 // VGPRs (2 waves/SIMD) without spilling.
-int spec_row_tile(size_t k, size_t m) {
+int spec_row_tile(size_t nin, size_t nout) {
     if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(16, atoi(e) & ~1));
     // split matrices: 8-row passes keep each program's straight-line passes
     // (and so its compile time) small
-    return k * m > 4096 ? 8 : gf_row_tile((int)m);
+    return nin * nout > 4096 ? 8 : gf_row_tile((int)nout);
 }
 
-// Load (or, with HBRBC_JIT=1, compile and cache) the specialised encoder.
-// Any failure leaves the context on the generic bit-sliced kernel.
-void drop_spec(hbrbc_ctx *c) {
-    for (auto &g : c->spec)
-        if (g.mod) (void)hipModuleUnload(g.mod);
-    c->spec.clear();
+// The encoder program of parity-row group [r_lo, r_hi) for row block rb.
+XorProgram encode_program(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
+                          int r_lo, int r_hi, int rb) {
+    XorProgram p;
+    p.name = encode_kernel_name(k, m, rt, depth, r_lo, rb);
+    for (size_t j = 0; j < k; ++j) p.in_rows.push_back((int)j);
+    for (int r = r_lo; r < r_hi; ++r) p.out_rows.push_back((int)(k + r));
+    p.coefs.assign(parity_rows + (size_t)r_lo * k, parity_rows + (size_t)r_hi * k);
+    p.rt = rt;
+    p.depth = depth;
+    p.rb = rb;
+    p.fused = true;
+    return p;
 }
 
-void setup_spec_encoder(hbrbc_ctx *c) {
-    const char *mode = getenv("HBRBC_JIT");
-    if (c->m == 0 || (mode && !std::strcmp(mode, "0")) || c->k * c->m > 16384) return;
-    c->rt_spec = spec_row_tile(c->k, c->m);
-    c->depth_spec = spec_depth();
-    for (const auto &rg : encode_groups(c->k, c->m, c->rt_spec)) {
-        const std::string path =
-            jit_file(jit_dir(), c->k, c->m, c->rt_spec, c->depth_spec, rg.first);
-        std::vector<char> code;
-        if (!read_file(path, code)) {
-            if (!mode || std::strcmp(mode, "1")) return drop_spec(c);
-            std::string log;
-            if (compile_encode(c->k, c->m, c->matrix.data() + c->k * c->k, c->rt_spec,
-                               c->depth_spec, rg.first, rg.second, code, log)) {
-                c->enc_kind = "jit-failed";
-                return drop_spec(c);
-            }
-            mkdir(jit_dir().c_str(), 0755);
-            if (FILE *f = fopen(path.c_str(), "wb")) {
-                fwrite(code.data(), 1, code.size(), f);
-                fclose(f);
-            }
-        }
-        hbrbc_ctx::SpecGroup g{rg.first, rg.second, nullptr, nullptr, nullptr};
-        if (hipModuleLoadData(&g.mod, code.data()) != hipSuccess) return drop_spec(c);
-        c->spec.push_back(g);
-        auto &b = c->spec.back();
-        if (hipModuleGetFunction(&b.enc, b.mod,
-                                 encode_kernel_name(c->k, c->m, c->rt_spec, c->depth_spec, false,
-                                                    rg.first)
-                                     .c_str()) != hipSuccess ||
-            hipModuleGetFunction(&b.fe, b.mod,
-                                 encode_kernel_name(c->k, c->m, c->rt_spec,
-                                                    fused_depth(c->depth_spec), true, rg.first)
-                                     .c_str()) != hipSuccess)
-            return drop_spec(c);
+// The decoder programs of one erasure pattern (output-row groups).
+bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const uint8_t *present,
+                     int rb, std::vector<XorProgram> &out, uint64_t &hash, int &rt) {
+    std::vector<int> valid, missing;
+    std::vector<uint8_t> rows;
+    if (!recovery_rows(mat, k, n, present, valid, missing, rows)) return false;
+    hash = pattern_hash(present, (int)n);
+    rt = spec_row_tile(k, missing.size());
+    const int depth = spec_depth();
+    const auto groups = xor_groups(k, missing.size(), rt);
+    out.clear();
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        XorProgram p;
+        p.name = decode_kernel_name(n, hash, rt, depth, (int)gi, rb);
+        p.in_rows = valid;
+        p.out_rows.assign(missing.begin() + groups[gi].first, missing.begin() + groups[gi].second);
+        p.coefs.assign(rows.begin() + (size_t)groups[gi].first * k,
+                       rows.begin() + (size_t)groups[gi].second * k);
+        p.rt = rt;
+        p.depth = depth;
+        p.rb = rb;
+        p.guard = hash;
+        out.push_back(std::move(p));
     }
-    c->enc_kind = "specialised";
+    return true;
 }
 
-// HBRBC_SPEC_SPLIT=1: launch the specialised encoder pass by pass.
+// Load the module of `p` from the cache (or, if allowed, compile and cache it).
+int load_program(const XorProgram &p, bool compile, hbrbc_ctx::SpecGroup &g) {
+    const std::string path = jit_file(jit_dir(), p.name);
+    std::vector<char> code;
+    if (!read_file(path, code)) {
+        if (!compile) return fail(HBRBC_E_INVALID_ARG, "no cached code object %s", path.c_str());
+        std::string log;
+        if (compile_source(gen_xor_source(p), code, log))
+            return fail(HBRBC_E_DEVICE, "hiprtc: %s", log.substr(0, 400).c_str());
+        mkdir(jit_dir().c_str(), 0755);
+        (void)write_file(path, code);
+    }
+    g.mod = nullptr;
+    g.fn = g.fe = nullptr;
+    HB_HIP(hipModuleLoadData(&g.mod, code.data()));
+    if (hipModuleGetFunction(&g.fn, g.mod, p.name.c_str()) != hipSuccess ||
+        (p.fused && hipModuleGetFunction(&g.fe, g.mod, (p.name + "_fe").c_str()) != hipSuccess)) {
+        (void)hipModuleUnload(g.mod);
+        g.mod = nullptr;
+        return fail(HBRBC_E_DEVICE, "kernel missing in %s", path.c_str());
+    }
+    return HBRBC_OK;
+}
+
+void drop_groups(std::vector<hbrbc_ctx::SpecGroup> &gs) {
+    for (auto &g : gs)
+        if (g.mod) (void)hipModuleUnload(g.mod);
+    gs.clear();
+}
+
+// The specialised encoder of this context for row block rb, loaded on first
+// use (or, with HBRBC_JIT=1, compiled and cached).  nullptr: use the generic
+// kernel.
+const std::vector<hbrbc_ctx::SpecGroup> *spec_encoder(hbrbc_ctx *c, int rb) {
+    auto it = c->enc_spec.find(rb);
+    if (it != c->enc_spec.end()) return it->second.empty() ? nullptr : &it->second;
+    std::vector<hbrbc_ctx::SpecGroup> gs;
+    const char *mode = getenv("HBRBC_JIT");
+    const bool off = c->m == 0 || (mode && !std::strcmp(mode, "0")) || c->k * c->m > 16384;
+    if (!off) {
+        const bool compile = mode && !std::strcmp(mode, "1");
+        const std::string saved = g_err;
+        for (const auto &rg : xor_groups(c->k, c->m, c->rt_spec)) {
+            const XorProgram p = encode_program(c->k, c->m, c->matrix.data() + c->k * c->k,
+                                                c->rt_spec, c->depth_spec, rg.first, rg.second, rb);
+            hbrbc_ctx::SpecGroup g{rg.first, rg.second, nullptr, nullptr, nullptr};
+            if (load_program(p, compile, g)) {
+                drop_groups(gs);
+                break;
+            }
+            gs.push_back(g);
+        }
+        g_err = saved;  // a missing code object is not an error of the caller's call
+    }
+    auto &slot = c->enc_spec[rb];
+    slot = std::move(gs);
+    return slot.empty() ? nullptr : &slot;
+}
+
+// HBRBC_SPEC_SPLIT=1: launch the specialised kernels pass by pass.
 bool spec_pass_split() {
     const char *e = getenv("HBRBC_SPEC_SPLIT");
     return e && !std::strcmp(e, "1");
 }
 
-// Launch one group's encode (fused = frame+encode twin of group 0).
-hipError_t launch_spec_group(hbrbc_ctx *c, const hbrbc_ctx::SpecGroup &g, bool fused,
-                             uint8_t *shards, size_t shard_len, size_t shard_stride,
-                             size_t inst_stride, size_t count, const uint8_t *payloads,
-                             size_t payload_stride, size_t payload_len, hipStream_t s) {
-    uint8_t *base = shards;
-    const uint8_t *pay = payloads;
-    unsigned long ist = inst_stride, sst = shard_stride, pst = payload_stride;
-    unsigned row_bytes = (unsigned)(fused ? shard_stride : round_up(shard_len, 16));
-    unsigned P = (unsigned)payload_len, S = (unsigned)shard_len;
-    unsigned wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
-    const size_t blocks = (size_t)wpr * count;
+hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, XorArgs a,
+                            size_t count, hipStream_t s) {
+    a.waves_per_row = (a.row_bytes + 64 * 32 - 1) / (64 * 32);
+    const size_t blocks = (size_t)a.waves_per_row * count;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const int npass = (g.r_hi - g.r_lo + c->rt_spec - 1) / c->rt_spec;
-    int p_only = -1;
-    void *args_e[] = {&base, &ist, &sst, &row_bytes, &wpr, &p_only};
-    void *args_f[] = {&base, &ist, &sst, &row_bytes, &wpr, &pay, &pst, &P, &S, &p_only};
-    void **args = fused ? args_f : args_e;
+    const int npass = (g.r_hi - g.r_lo + rt - 1) / rt;
+    void *args[] = {&a.base,     &a.inst_stride, &a.shard_stride, &a.block_stride,
+                    &a.row_bytes, &a.waves_per_row, &a.payloads,  &a.payload_stride,
+                    &a.P,        &a.S,           &a.pat,          &a.slot_hash,
+                    &a.hash_slots, &a.p_only};
+    hipFunction_t fn = fused ? g.fe : g.fn;
     if (!spec_pass_split()) {
+        a.p_only = -1;
         const unsigned threads = 64u * (unsigned)std::min(4, npass);
-        return hipModuleLaunchKernel(fused ? g.fe : g.enc, (unsigned)blocks, 1, 1, threads, 1, 1, 0,
-                                     s, args, nullptr);
+        return hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args, nullptr);
     }
     // one launch per pass, one wave per workgroup: every wave on the chip
     // runs the same pass's code (the three-pass N = 64 program is 151 KB of
     // straight-line code, more than the instruction cache a CU pair shares)
-    for (p_only = 0; p_only < npass; ++p_only) {
-        const hipError_t e = hipModuleLaunchKernel(fused ? g.fe : g.enc, (unsigned)blocks, 1, 1, 64u,
-                                                   1, 1, 0, s, args, nullptr);
+    for (a.p_only = 0; a.p_only < npass; ++a.p_only) {
+        const hipError_t e = hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 64u, 1, 1, 0, s, args,
+                                                   nullptr);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -485,13 +711,101 @@ hbrbc_ctx *default_ctx(int *st) {
     return g_default;
 }
 
+// Generic (bit-sliced) encode of parity rows k..n-1 in the given layout.
+int generic_encode(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &rows,
+                   size_t inst_stride, size_t count, hipStream_t s) {
+    GfApplyArgs g{};
+    g.base = shards;
+    g.inst_stride = inst_stride;
+    g.rows = rows;
+    g.n16 = (int)((shard_len + 15) / 16);
+    g.coefs = c->d_enc_coefs.as<uint8_t>();
+    g.coef_slot_stride = 0;
+    g.in_idx = c->d_enc_in.as<uint32_t>();
+    g.in_idx_stride = 0;
+    g.out_idx = c->d_enc_out.as<uint32_t>();
+    g.out_idx_stride = 0;
+    g.nout = nullptr;
+    g.nout_uniform = (int)c->m;
+    g.pat = nullptr;
+    g.max_rows = (int)c->m;
+    g.nin = (int)c->k;
+    g.rt = c->rt_enc;
+    g.mode = c->gf_mode;
+    g.count = count;
+    HB_HIP(launch_gf_apply(g, s));
+    return HBRBC_OK;
+}
+
+int encode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &rows,
+                size_t inst_stride, size_t count, hipStream_t s) {
+    StageTimer t(c, HBRBC_STAGE_ENCODE, s);
+    if (const auto *gs = spec_encoder(c, code_rb(rows))) {
+        // specialised XOR networks (jit.hip), one launch per parity-row group
+        XorArgs x{};
+        x.base = shards;
+        x.inst_stride = inst_stride;
+        x.shard_stride = rows.sst;
+        x.block_stride = rows.bst;
+        x.row_bytes = (unsigned)round_up(shard_len, 16);
+        x.p_only = -1;
+        for (const auto &grp : *gs) HB_HIP(launch_xor_group(grp, false, c->rt_spec, x, count, s));
+        return HBRBC_OK;
+    }
+    return generic_encode(c, shards, shard_len, rows, inst_stride, count, s);
+}
+
+int frame_rows(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stride, size_t payload_len,
+               size_t count, uint8_t *shards, size_t shard_len, const RowMap &rows,
+               size_t inst_stride, hipStream_t s) {
+    StageTimer t(c, HBRBC_STAGE_FRAME, s);
+    HB_HIP(launch_frame(payloads, payload_stride, payload_len, count, shards, shard_len, rows,
+                        inst_stride, c->k, s));
+    return HBRBC_OK;
+}
+
+int check_payloads(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stride,
+                   size_t payload_len, size_t shard_len) {
+    if (shard_len != hbrbc_shard_len(payload_len, c->k))
+        return fail(HBRBC_E_INVALID_ARG, "shard_len %zu != ceil((%zu+4)/%zu)", shard_len,
+                    payload_len, c->k);
+    if (payload_len > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "payload too large");
+    if (payload_len && (!payloads || reinterpret_cast<uintptr_t>(payloads) % 4 ||
+                        payload_stride % 4 || payload_stride < round_up(payload_len, 4)))
+        return fail(HBRBC_E_INVALID_ARG, "payload buffer must be 4-byte aligned with stride >= "
+                                         "round_up(len, 4)");
+    return HBRBC_OK;
+}
+
+int decode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &rows,
+                size_t inst_stride, const uint8_t *present, size_t count, const uint8_t *roots,
+                size_t root_stride, uint8_t *nodes, size_t node_inst_stride, bool known_leaves,
+                uint8_t *payload_out, size_t payload_stride, uint32_t *payload_len_out,
+                int32_t *status_out, hipStream_t s) {
+    int st = ensure_workspace(c, count);
+    if (st) return st;
+    int32_t *rstat = c->ws_status.as<int32_t>();
+    st = run_reconstruct(c, shards, shard_len, rows, inst_stride, present, count, rstat, s);
+    if (st) return st;
+    st = run_merkle(c, shards, shard_len, rows, inst_stride, c->n, count, nodes, node_inst_stride,
+                    known_leaves, s);
+    if (st) return st;
+    StageTimer t(c, HBRBC_STAGE_UNFRAME, s);
+    HB_HIP(launch_decode_check(rstat, nodes, node_inst_stride, hbrbc_merkle_node_count(c->n) - 1,
+                               roots, root_stride, shards, shard_len, rows, inst_stride, c->k,
+                               count, payload_len_out, status_out, s));
+    HB_HIP(launch_unframe(shards, shard_len, rows, inst_stride, c->k, count, payload_len_out,
+                          status_out, payload_out, payload_stride, s));
+    return HBRBC_OK;
+}
+
 }  // namespace
 
 // =========================================================================
 extern "C" {
 
 const char *hbrbc_last_error(void) { return g_err.c_str(); }
-const char *hbrbc_version(void) { return "hbrbc 0.1.0 gfx950"; }
+const char *hbrbc_version(void) { return "hbrbc 0.2.0 gfx950"; }
 
 int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc_ctx **out) {
     if (!out) return fail(HBRBC_E_INVALID_ARG, "out is null");
@@ -532,11 +846,10 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
     }
     if (const char *e = getenv("HBRBC_GF")) {
         // bitslice (uniform branches), bitslice_likely (set-bit path inline),
-        // bitslice_mask (branch-free masked xor), perm (split-2-bit v_perm)
-        if (!std::strcmp(e, "perm")) c->bitslice = 0;
-        else if (!std::strcmp(e, "bitslice_likely")) c->bitslice = 2;
-        else if (!std::strcmp(e, "bitslice_mask")) c->bitslice = 3;
-        else c->bitslice = 1;
+        // bitslice_mask (branch-free masked xor)
+        if (!std::strcmp(e, "bitslice_likely")) c->gf_mode = 1;
+        else if (!std::strcmp(e, "bitslice_mask")) c->gf_mode = 2;
+        else c->gf_mode = 0;
     }
     if (const char *e = getenv("HBRBC_RT_ENC")) c->rt_enc = std::max(2, std::min(16, atoi(e) & ~1));
     if (const char *e = getenv("HBRBC_RT_REC")) c->rt_rec = std::max(2, std::min(16, atoi(e) & ~1));
@@ -554,29 +867,20 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
     if (st == HBRBC_OK)
         guard(hipMemcpy(c->d_matrix.p, c->matrix.data(), c->matrix.size(), hipMemcpyHostToDevice));
     if (c->m > 0 && st == HBRBC_OK) {
-        const HostGf &g = gf();
-        // pass-major tables, zero-padded rows: split-2-bit entries [pass][j][rt_enc]
-        // (v_perm kernel) or coefficient bytes [pass][j][16] (bit-sliced kernel)
+        // pass-major coefficient bytes [pass][j][16], zero-padded rows
         const size_t rt = (size_t)c->rt_enc, npass = (c->m + rt - 1) / rt;
-        std::vector<uint4> tab(npass * rt * c->k, make_uint4(0, 0, 0, 0));
-        uint8_t *raw = reinterpret_cast<uint8_t *>(tab.data());
+        std::vector<uint8_t> tab(npass * c->k * 16, 0);
         for (size_t r = 0; r < c->m; ++r)
-            for (size_t j = 0; j < c->k; ++j) {
-                const uint8_t coef = c->matrix[(c->k + r) * c->k + j];
-                if (c->bitslice)
-                    raw[((r / rt) * c->k + j) * 16 + (r % rt)] = coef;
-                else
-                    tab[((r / rt) * c->k + j) * rt + (r % rt)] = gf_split2_entry(coef, g.exp, g.log);
-            }
+            for (size_t j = 0; j < c->k; ++j)
+                tab[((r / rt) * c->k + j) * 16 + (r % rt)] = c->matrix[(c->k + r) * c->k + j];
         std::vector<uint32_t> in(c->k), outi(c->m);
         for (size_t j = 0; j < c->k; ++j) in[j] = (uint32_t)j;
         for (size_t r = 0; r < c->m; ++r) outi[r] = (uint32_t)(c->k + r);
-        guard(c->d_enc_tables.ensure(tab.size() * sizeof(uint4)));
+        guard(c->d_enc_coefs.ensure(tab.size()));
         guard(c->d_enc_in.ensure(in.size() * sizeof(uint32_t)));
         guard(c->d_enc_out.ensure(outi.size() * sizeof(uint32_t)));
         if (st == HBRBC_OK) {
-            guard(hipMemcpy(c->d_enc_tables.p, tab.data(), tab.size() * sizeof(uint4),
-                            hipMemcpyHostToDevice));
+            guard(hipMemcpy(c->d_enc_coefs.p, tab.data(), tab.size(), hipMemcpyHostToDevice));
             guard(hipMemcpy(c->d_enc_in.p, in.data(), in.size() * sizeof(uint32_t),
                             hipMemcpyHostToDevice));
             guard(hipMemcpy(c->d_enc_out.p, outi.data(), outi.size() * sizeof(uint32_t),
@@ -587,8 +891,13 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
         hbrbc_coding_free(c);
         return st;
     }
-    c->enc_kind = c->m == 0 ? "trivial" : (c->bitslice ? "bitslice" : "perm");
-    if (c->bitslice) setup_spec_encoder(c);
+    c->rt_spec = spec_row_tile(c->k, c->m);
+    c->depth_spec = spec_depth();
+    c->enc_kind = c->m == 0 ? "trivial" : (spec_encoder(c, 256) ? "specialised" : "bitslice");
+    if (c->m > 0 && c->enc_kind == "bitslice") {
+        const char *mode = getenv("HBRBC_JIT");
+        if (mode && !std::strcmp(mode, "1") && c->k * c->m <= 16384) c->enc_kind = "jit-failed";
+    }
     *out = c;
     return HBRBC_OK;
 }
@@ -597,13 +906,15 @@ void hbrbc_coding_free(hbrbc_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->d_matrix, &c->d_enc_tables, &c->d_enc_in, &c->d_enc_out, &c->ws_tables,
-                      &c->ws_in, &c->ws_out, &c->ws_nout, &c->ws_status, &c->ws_plen, &c->st_slab,
-                      &c->st_present, &c->st_status, &c->st_nodes, &c->st_aux, &c->st_aux2,
-                      &c->st_aux3})
+    for (DevBuf *b : {&c->d_matrix, &c->d_enc_coefs, &c->d_enc_in, &c->d_enc_out, &c->pc_hash,
+                      &c->pc_keys, &c->pc_coefs, &c->pc_in, &c->pc_out, &c->pc_nout, &c->pc_status,
+                      &c->pc_fill, &c->ws_pat, &c->ws_own, &c->ws_status, &c->ws_list,
+                      &c->ws_counter, &c->st_slab, &c->st_nodes, &c->st_aux})
         b->release();
+    c->pin.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    drop_spec(c);
+    for (auto &kv : c->enc_spec) drop_groups(kv.second);
+    for (auto &kv : c->dec_spec) drop_groups(kv.second.groups);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -647,22 +958,13 @@ int hbrbc_frame_batch(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stri
                       size_t shard_stride, size_t inst_stride, void *stream) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (count == 0) return HBRBC_OK;
-    if (shard_len != hbrbc_shard_len(payload_len, c->k))
-        return fail(HBRBC_E_INVALID_ARG, "shard_len %zu != ceil((%zu+4)/%zu)", shard_len,
-                    payload_len, c->k);
-    if (payload_len > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "payload too large");
-    if (payload_len && (!payloads || reinterpret_cast<uintptr_t>(payloads) % 4 ||
-                        payload_stride % 4 || payload_stride < round_up(payload_len, 4)))
-        return fail(HBRBC_E_INVALID_ARG, "payload buffer must be 4-byte aligned with stride >= "
-                                         "round_up(len, 4)");
-    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
+    int st = check_payloads(c, payloads, payload_stride, payload_len, shard_len);
+    if (st) return st;
+    st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
     if (st) return st;
     HB_HIP(hipSetDevice(c->device));
-    hipStream_t s = pick(c, stream);
-    StageTimer t(c, HBRBC_STAGE_FRAME, s);
-    HB_HIP(launch_frame(payloads, payload_stride, payload_len, count, shards, shard_len,
-                        shard_stride, inst_stride, c->k, s));
-    return HBRBC_OK;
+    return frame_rows(c, payloads, payload_stride, payload_len, count, shards, shard_len,
+                      plain_rows(shard_stride), inst_stride, pick(c, stream));
 }
 
 int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
@@ -673,88 +975,88 @@ int hbrbc_encode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
     if (st) return st;
     HB_HIP(hipSetDevice(c->device));
+    return encode_rows(c, shards, shard_len, plain_rows(shard_stride), inst_stride, count,
+                       pick(c, stream));
+}
+
+int hbrbc_frame_encode_rows(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stride,
+                            size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
+                            size_t shard_stride, size_t rows_per_block, size_t block_stride,
+                            size_t inst_stride, void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (count == 0) return HBRBC_OK;
+    int st = check_payloads(c, payloads, payload_stride, payload_len, shard_len);
+    if (st) return st;
+    st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count, rows_per_block,
+                    block_stride);
+    if (st) return st;
+    HB_HIP(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
-    StageTimer t(c, HBRBC_STAGE_ENCODE, s);
-    if (!c->spec.empty()) {
-        // specialised XOR networks (jit.hip), one launch per parity-row group
-        for (const auto &grp : c->spec)
-            HB_HIP(launch_spec_group(c, grp, false, shards, shard_len, shard_stride, inst_stride,
-                                     count, nullptr, 0, 0, s));
-        return HBRBC_OK;
+    const RowMap rows = make_rows(c->n, shard_stride, rows_per_block, block_stride);
+    const std::vector<hbrbc_ctx::SpecGroup> *gs = nullptr;
+    if (c->m > 0 && shard_stride == round_up(shard_len, 16) && payload_len <= 0x7FFFFFFFull &&
+        shard_len * c->k < 0x7FFFFFFFull)
+        gs = spec_encoder(c, code_rb(rows));
+    if (!gs) {
+        st = frame_rows(c, payloads, payload_stride, payload_len, count, shards, shard_len, rows,
+                        inst_stride, s);
+        if (st || c->m == 0) return st;
+        return encode_rows(c, shards, shard_len, rows, inst_stride, count, s);
     }
-    GfApplyArgs g;
-    g.base = shards;
-    g.inst_stride = inst_stride;
-    g.shard_stride = shard_stride;
-    g.n16 = (int)((shard_len + 15) / 16);
-    g.tables = c->d_enc_tables.as<uint4>();
-    g.tab_inst_stride = 0;
-    g.rt = c->rt_enc;
-    g.bitslice = c->bitslice;
-    g.in_idx = c->d_enc_in.as<uint32_t>();
-    g.in_idx_stride = 0;
-    g.out_idx = c->d_enc_out.as<uint32_t>();
-    g.out_idx_stride = 0;
-    g.nout = nullptr;
-    g.nout_uniform = (int)c->m;
-    g.max_rows = (int)c->m;
-    g.nin = (int)c->k;
-    g.count = count;
-    HB_HIP(launch_gf_apply(g, s));
+    StageTimer t(c, HBRBC_STAGE_ENCODE, s);
+    // frame folded into the specialised encoder (jit.hip): group 0's twin
+    // writes the framed data rows and its parity rows, the fixup adds the
+    // last partial payload dword to both, and the other groups then encode
+    // from the complete data rows
+    XorArgs x{};
+    x.base = shards;
+    x.inst_stride = inst_stride;
+    x.shard_stride = rows.sst;
+    x.block_stride = rows.bst;
+    x.row_bytes = (unsigned)shard_stride;
+    x.payloads = payloads;
+    x.payload_stride = payload_stride;
+    x.P = (unsigned)payload_len;
+    x.S = (unsigned)shard_len;
+    x.p_only = -1;
+    const auto &g0 = gs->front();
+    HB_HIP(launch_xor_group(g0, true, c->rt_spec, x, count, s));
+    HB_HIP(launch_frame_fixup(payloads, payload_stride, payload_len, shards, shard_len, rows,
+                              inst_stride, c->k, (size_t)g0.r_hi, c->d_matrix.as<uint8_t>(), count,
+                              s));
+    for (size_t i = 1; i < gs->size(); ++i)
+        HB_HIP(launch_xor_group((*gs)[i], false, c->rt_spec, x, count, s));
     return HBRBC_OK;
 }
 
 int hbrbc_frame_encode_batch(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stride,
                              size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
                              size_t shard_stride, size_t inst_stride, void *stream) {
+    return hbrbc_frame_encode_rows(c, payloads, payload_stride, payload_len, count, shards,
+                                   shard_len, shard_stride, 0, 0, inst_stride, stream);
+}
+
+int hbrbc_merkle_rows(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, size_t shard_stride,
+                      size_t rows_per_block, size_t block_stride, size_t inst_stride, size_t count,
+                      uint8_t *nodes, size_t node_inst_stride, void *stream) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (count == 0) return HBRBC_OK;
-    const bool fused = !c->spec.empty() && shard_stride == round_up(shard_len, 16) &&
-                       shard_len == hbrbc_shard_len(payload_len, c->k) &&
-                       payload_len <= 0x7FFFFFFFull && shard_len * c->k < 0x7FFFFFFFull;
-    if (!fused) {
-        int st = hbrbc_frame_batch(c, payloads, payload_stride, payload_len, count, shards,
-                                   shard_len, shard_stride, inst_stride, stream);
-        return st ? st : hbrbc_encode_batch(c, shards, shard_len, shard_stride, inst_stride, count,
-                                            stream);
-    }
-    if (payload_len && (!payloads || reinterpret_cast<uintptr_t>(payloads) % 4 ||
-                        payload_stride % 4 || payload_stride < round_up(payload_len, 4)))
-        return fail(HBRBC_E_INVALID_ARG, "payload buffer must be 4-byte aligned with stride >= "
-                                         "round_up(len, 4)");
-    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
+    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count, rows_per_block,
+                        block_stride);
+    if (st) return st;
+    st = check_nodes(nodes, node_inst_stride, c->n, count);
     if (st) return st;
     HB_HIP(hipSetDevice(c->device));
-    hipStream_t s = pick(c, stream);
-    StageTimer t(c, HBRBC_STAGE_ENCODE, s);
-    // frame folded into the specialised encoder (jit.hip): group 0's twin
-    // writes the framed data rows and its parity rows, the fixup adds the
-    // last partial payload dword to both, and the other groups then encode
-    // from the complete data rows
-    const auto &g0 = c->spec.front();
-    HB_HIP(launch_spec_group(c, g0, true, shards, shard_len, shard_stride, inst_stride, count,
-                             payloads, payload_stride, payload_len, s));
-    HB_HIP(launch_frame_fixup(payloads, payload_stride, payload_len, shards, shard_len,
-                              shard_stride, inst_stride, c->k, (size_t)g0.r_hi,
-                              c->d_matrix.as<uint8_t>(), count, s));
-    for (size_t i = 1; i < c->spec.size(); ++i)
-        HB_HIP(launch_spec_group(c, c->spec[i], false, shards, shard_len, shard_stride,
-                                 inst_stride, count, nullptr, 0, 0, s));
-    return HBRBC_OK;
+    return run_merkle(c, shards, shard_len,
+                      make_rows(c->n, shard_stride, rows_per_block, block_stride), inst_stride,
+                      c->n, count, nodes, node_inst_stride, false, pick(c, stream));
 }
 
 int hbrbc_merkle_batch(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len,
                        size_t shard_stride, size_t inst_stride, size_t count, uint8_t *nodes,
                        size_t node_inst_stride, void *stream) {
-    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
-    if (count == 0) return HBRBC_OK;
-    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
-    if (st) return st;
-    st = check_nodes(nodes, node_inst_stride, c->n, count);
-    if (st) return st;
-    HB_HIP(hipSetDevice(c->device));
-    return run_merkle(c, shards, shard_len, shard_stride, inst_stride, c->n, count, nodes,
-                      node_inst_stride, pick(c, stream));
+    return hbrbc_merkle_rows(c, shards, shard_len, shard_stride, 0, 0, inst_stride, count, nodes,
+                             node_inst_stride, stream);
 }
 
 int hbrbc_proofs_batch(hbrbc_ctx *c, const uint8_t *nodes, size_t node_inst_stride, size_t count,
@@ -773,20 +1075,28 @@ int hbrbc_proofs_batch(hbrbc_ctx *c, const uint8_t *nodes, size_t node_inst_stri
     return HBRBC_OK;
 }
 
-int hbrbc_validate_batch(hbrbc_ctx *c, const uint8_t *values, size_t value_len,
-                         size_t value_stride, size_t value_inst_stride, size_t per_inst,
-                         const uint32_t *indices, const uint8_t *digests, const uint8_t *ndig,
-                         const uint8_t *roots, size_t root_stride, size_t tree_n, size_t count,
-                         uint8_t *ok_out, void *stream) {
+int hbrbc_validate_rows(hbrbc_ctx *c, const uint8_t *values, size_t value_len,
+                        size_t value_stride, size_t rows_per_block, size_t block_stride,
+                        size_t value_inst_stride, size_t per_inst, const uint32_t *rows,
+                        const uint32_t *indices, const uint8_t *digests, const uint8_t *ndig,
+                        size_t digest_rows, const uint8_t *roots, size_t root_stride,
+                        size_t tree_n, size_t count, uint8_t *ok_out, uint8_t *leaf_out,
+                        size_t leaf_inst_stride, void *stream) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (count == 0 || per_inst == 0) return HBRBC_OK;
     if (!values || reinterpret_cast<uintptr_t>(values) % 8 || value_stride % 8 ||
-        value_inst_stride % 8)
+        value_inst_stride % 8 || block_stride % 8)
         return fail(HBRBC_E_INVALID_ARG, "values must be 8-byte aligned with 8-byte strides");
     if (!ndig || !roots || !ok_out || reinterpret_cast<uintptr_t>(roots) % 16 || root_stride % 16)
         return fail(HBRBC_E_INVALID_ARG, "roots must be 16-byte aligned; outputs non-null");
     if (tree_n == 0 || tree_n > 0xFFFFFFFFull || value_len > 0xFFFFFFFFull)
         return fail(HBRBC_E_INVALID_ARG, "bad tree_n / value_len");
+    if (rows_per_block > 255 && rows_per_block < tree_n)
+        return fail(HBRBC_E_INVALID_ARG, "rows_per_block %zu > 255", rows_per_block);
+    if (rows && digest_rows == 0)
+        return fail(HBRBC_E_INVALID_ARG, "a row list needs digest_rows > every listed row");
+    if (leaf_out && (reinterpret_cast<uintptr_t>(leaf_out) % 16 || leaf_inst_stride % 16))
+        return fail(HBRBC_E_INVALID_ARG, "leaf_out must be 16-byte aligned");
     const size_t dslots = hbrbc_merkle_max_proof_len(tree_n);
     if (dslots && (!digests || reinterpret_cast<uintptr_t>(digests) % 16))
         return fail(HBRBC_E_INVALID_ARG, "digests must be 16-byte aligned");
@@ -796,20 +1106,34 @@ int hbrbc_validate_batch(hbrbc_ctx *c, const uint8_t *values, size_t value_len,
     ValidateArgs a;
     a.values = values;
     a.value_len = value_len;
-    a.value_stride = value_stride;
     a.value_inst_stride = value_inst_stride;
     a.per_inst = per_inst;
+    a.vrows = make_rows(tree_n, value_stride, rows_per_block, block_stride);
+    a.rows = rows;
     a.indices = indices;
     a.digests = digests;
     a.dslots = dslots;
+    a.dig_rows = rows ? digest_rows : per_inst;
     a.ndig = ndig;
     a.roots = roots;
     a.root_stride = root_stride;
     a.tree_n = tree_n;
     a.count = count;
     a.ok_out = ok_out;
+    a.leaf_out = leaf_out;
+    a.leaf_inst_stride = leaf_inst_stride;
     HB_HIP(launch_validate(a, s));
     return HBRBC_OK;
+}
+
+int hbrbc_validate_batch(hbrbc_ctx *c, const uint8_t *values, size_t value_len,
+                         size_t value_stride, size_t value_inst_stride, size_t per_inst,
+                         const uint32_t *indices, const uint8_t *digests, const uint8_t *ndig,
+                         const uint8_t *roots, size_t root_stride, size_t tree_n, size_t count,
+                         uint8_t *ok_out, void *stream) {
+    return hbrbc_validate_rows(c, values, value_len, value_stride, 0, 0, value_inst_stride,
+                               per_inst, nullptr, indices, digests, ndig, per_inst, roots,
+                               root_stride, tree_n, count, ok_out, nullptr, 0, stream);
 }
 
 int hbrbc_reserve(hbrbc_ctx *c, size_t count) {
@@ -818,25 +1142,36 @@ int hbrbc_reserve(hbrbc_ctx *c, size_t count) {
     return ensure_workspace(c, count);
 }
 
-int hbrbc_reconstruct_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
-                            size_t inst_stride, const uint8_t *present, size_t count,
-                            int32_t *status_out, void *stream) {
+int hbrbc_reconstruct_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                           size_t rows_per_block, size_t block_stride, size_t inst_stride,
+                           const uint8_t *present, size_t count, int32_t *status_out,
+                           void *stream) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (count == 0) return HBRBC_OK;
     if (!present || !status_out) return fail(HBRBC_E_INVALID_ARG, "null present/status");
     if (c->m > 0 && shard_len == 0) return fail(HBRBC_E_EMPTY_SHARD, "empty shards");
-    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
+    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count, rows_per_block,
+                        block_stride);
     if (st) return st;
     HB_HIP(hipSetDevice(c->device));
-    return run_reconstruct(c, shards, shard_len, shard_stride, inst_stride, present, count,
-                           status_out, pick(c, stream));
+    return run_reconstruct(c, shards, shard_len,
+                           make_rows(c->n, shard_stride, rows_per_block, block_stride),
+                           inst_stride, present, count, status_out, pick(c, stream));
 }
 
-int hbrbc_decode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
-                       size_t inst_stride, const uint8_t *present, size_t count,
-                       const uint8_t *roots, size_t root_stride, uint8_t *nodes,
-                       size_t node_inst_stride, uint8_t *payload_out, size_t payload_stride,
-                       uint32_t *payload_len_out, int32_t *status_out, void *stream) {
+int hbrbc_reconstruct_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                            size_t inst_stride, const uint8_t *present, size_t count,
+                            int32_t *status_out, void *stream) {
+    return hbrbc_reconstruct_rows(c, shards, shard_len, shard_stride, 0, 0, inst_stride, present,
+                                  count, status_out, stream);
+}
+
+int hbrbc_decode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                      size_t rows_per_block, size_t block_stride, size_t inst_stride,
+                      const uint8_t *present, size_t count, const uint8_t *roots,
+                      size_t root_stride, uint8_t *nodes, size_t node_inst_stride,
+                      int known_leaves, uint8_t *payload_out, size_t payload_stride,
+                      uint32_t *payload_len_out, int32_t *status_out, void *stream) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (count == 0) return HBRBC_OK;
     if (!present || !status_out || !payload_len_out || !roots)
@@ -844,7 +1179,8 @@ int hbrbc_decode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
     if (reinterpret_cast<uintptr_t>(roots) % 16 || root_stride % 16)
         return fail(HBRBC_E_INVALID_ARG, "roots must be 16-byte aligned");
     if (shard_len == 0) return fail(HBRBC_E_EMPTY_SHARD, "empty shards");
-    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count);
+    int st = check_slab(shards, shard_len, shard_stride, inst_stride, c->n, count, rows_per_block,
+                        block_stride);
     if (st) return st;
     st = check_nodes(nodes, node_inst_stride, c->n, count);
     if (st) return st;
@@ -855,25 +1191,120 @@ int hbrbc_decode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
         return fail(HBRBC_E_INVALID_ARG, "payload_out stride must be a multiple of 4 and >= %zu",
                     need);
     HB_HIP(hipSetDevice(c->device));
-    hipStream_t s = pick(c, stream);
-    st = ensure_workspace(c, count);
-    if (st) return st;
-    int32_t *rstat = c->ws_status.as<int32_t>();
-    st = run_reconstruct(c, shards, shard_len, shard_stride, inst_stride, present, count, rstat, s);
-    if (st) return st;
-    st = run_merkle(c, shards, shard_len, shard_stride, inst_stride, c->n, count, nodes,
-                    node_inst_stride, s);
-    if (st) return st;
-    StageTimer t(c, HBRBC_STAGE_UNFRAME, s);
-    HB_HIP(launch_decode_check(rstat, nodes, node_inst_stride, hbrbc_merkle_node_count(c->n) - 1,
-                               roots, root_stride, shards, shard_len, shard_stride, inst_stride,
-                               c->k, count, payload_len_out, status_out, s));
-    HB_HIP(launch_unframe(shards, shard_len, shard_stride, inst_stride, c->k, count,
-                          payload_len_out, status_out, payload_out, payload_stride, s));
+    return decode_rows(c, shards, shard_len,
+                       make_rows(c->n, shard_stride, rows_per_block, block_stride), inst_stride,
+                       present, count, roots, root_stride, nodes, node_inst_stride,
+                       known_leaves != 0, payload_out, payload_stride, payload_len_out,
+                       status_out, pick(c, stream));
+}
+
+int hbrbc_decode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                       size_t inst_stride, const uint8_t *present, size_t count,
+                       const uint8_t *roots, size_t root_stride, uint8_t *nodes,
+                       size_t node_inst_stride, uint8_t *payload_out, size_t payload_stride,
+                       uint32_t *payload_len_out, int32_t *status_out, void *stream) {
+    return hbrbc_decode_rows(c, shards, shard_len, shard_stride, 0, 0, inst_stride, present, count,
+                             roots, root_stride, nodes, node_inst_stride, 0, payload_out,
+                             payload_stride, payload_len_out, status_out, stream);
+}
+
+// ---------------------------------------------------- decode-matrix cache --
+int hbrbc_decode_cache_clear(hbrbc_ctx *c) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (!c->pc_cap) return HBRBC_OK;
+    HB_HIP(hipSetDevice(c->device));
+    HB_HIP(hipDeviceSynchronize());
+    HB_HIP(hipMemset(c->pc_hash.p, 0, (size_t)c->pc_cap * sizeof(uint64_t)));
+    HB_HIP(hipMemset(c->pc_fill.p, 0, sizeof(uint32_t)));
+    c->pc_inserted = 0;
     return HBRBC_OK;
 }
 
+int hbrbc_decode_cache_fill(hbrbc_ctx *c, uint32_t *patterns_out) {
+    if (!c || !patterns_out) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    *patterns_out = 0;
+    if (!c->pc_cap) return HBRBC_OK;
+    HB_HIP(hipSetDevice(c->device));
+    HB_HIP(hipDeviceSynchronize());
+    HB_HIP(hipMemcpy(patterns_out, c->pc_fill.p, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return HBRBC_OK;
+}
+
+int hbrbc_decoder_specialise(hbrbc_ctx *c, const uint8_t *present, size_t rows_per_block) {
+    if (!c || !present) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    if (c->m == 0) return HBRBC_OK;  // Coding::Trivial rebuilds nothing
+    HB_HIP(hipSetDevice(c->device));
+    const int rb = (rows_per_block && rows_per_block < c->n) ? (int)rows_per_block : 256;
+    if (rb > 255 && rb != 256) return fail(HBRBC_E_INVALID_ARG, "rows_per_block > 255");
+    std::vector<XorProgram> progs;
+    uint64_t hash = 0;
+    int rt = 2;
+    if (!decode_programs(c->matrix, c->k, c->n, present, rb, progs, hash, rt))
+        return fail(HBRBC_E_INVALID_ARG, "pattern has nothing to rebuild or too few shards");
+    const char *mode = getenv("HBRBC_JIT");
+    const bool compile = !(mode && !std::strcmp(mode, "0"));
+    hbrbc_ctx::DecSpec d;
+    d.hash = hash;
+    d.rt = rt;
+    int ng = 0;
+    for (const auto &p : progs) {
+        hbrbc_ctx::SpecGroup g{0, (int)p.out_rows.size(), nullptr, nullptr, nullptr};
+        (void)ng;
+        const int st = load_program(p, compile, g);
+        if (st) {
+            drop_groups(d.groups);
+            return st;
+        }
+        d.groups.push_back(g);
+    }
+    HB_HIP(hipDeviceSynchronize());  // no launch of the previous decoder is in flight
+    auto it = c->dec_spec.find(rb);
+    if (it != c->dec_spec.end()) drop_groups(it->second.groups);
+    c->dec_spec[rb] = std::move(d);
+    return HBRBC_OK;
+}
+
+size_t hbrbc_jit_decode_groups(size_t data_shards, size_t parity_shards, const uint8_t *present) {
+    std::vector<uint8_t> mat;
+    const size_t n = data_shards + parity_shards;
+    if (!present || data_shards == 0 || n > 256 || !build_matrix(data_shards, n, mat)) return 0;
+    std::vector<XorProgram> progs;
+    uint64_t hash;
+    int rt;
+    return decode_programs(mat, data_shards, n, present, 256, progs, hash, rt) ? progs.size() : 0;
+}
+
+int hbrbc_jit_build_decode(size_t data_shards, size_t parity_shards, const uint8_t *present,
+                           size_t rows_per_block, size_t group, const char *dir) {
+    std::vector<uint8_t> mat;
+    const size_t n = data_shards + parity_shards;
+    if (!present || data_shards == 0 || n > 256)
+        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, data + parity <= 256, a pattern");
+    if (!build_matrix(data_shards, n, mat))
+        return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
+    const int rb = (rows_per_block && rows_per_block < n) ? (int)rows_per_block : 256;
+    std::vector<XorProgram> progs;
+    uint64_t hash;
+    int rt;
+    if (!decode_programs(mat, data_shards, n, present, rb, progs, hash, rt))
+        return fail(HBRBC_E_INVALID_ARG, "pattern has nothing to rebuild or too few shards");
+    if (group >= progs.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group, progs.size());
+    std::vector<char> code;
+    std::string log;
+    if (compile_source(gen_xor_source(progs[group]), code, log))
+        return fail(HBRBC_E_DEVICE, "hiprtc: %s", log.substr(0, 400).c_str());
+    const std::string d = dir ? std::string(dir) : jit_dir();
+    mkdir(d.c_str(), 0755);
+    const std::string path = jit_file(d, progs[group].name);
+    return write_file(path, code) ? HBRBC_OK
+                                  : fail(HBRBC_E_INVALID_ARG, "cannot write %s", path.c_str());
+}
+
 // ---------------------------------------------------------------- layer 1 --
+// The per-call shims stage through one pinned host buffer per context: one
+// host-to-device DMA of everything the kernel reads, one device-to-host DMA
+// of the results, one stream synchronisation (the shim mutex serialises
+// calls that share the context's staging).
 int hbrbc_encode(hbrbc_ctx *c, uint8_t *const *shards, const size_t *lens, size_t n_shards) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     if (c->m == 0) return HBRBC_OK;  // Coding::Trivial::encode -> Ok(())
@@ -889,14 +1320,19 @@ int hbrbc_encode(hbrbc_ctx *c, uint8_t *const *shards, const size_t *lens, size_
     HB_HIP(hipSetDevice(c->device));
     const size_t stride = round_up(len, 16);
     HB_HIP(c->st_slab.ensure(c->n * stride));
-    uint8_t *slab = c->st_slab.as<uint8_t>();
-    for (size_t j = 0; j < c->k; ++j)
-        HB_HIP(hipMemcpyAsync(slab + j * stride, shards[j], len, hipMemcpyHostToDevice, c->stream));
-    int st = hbrbc_encode_batch(c, slab, len, stride, c->n * stride, 1, c->stream);
+    HB_HIP(c->pin.ensure(c->n * stride));
+    uint8_t *slab = c->st_slab.as<uint8_t>(), *pin = c->pin.as<uint8_t>();
+    for (size_t j = 0; j < c->k; ++j) {
+        std::memcpy(pin + j * stride, shards[j], len);
+        std::memset(pin + j * stride + len, 0, stride - len);
+    }
+    HB_HIP(hipMemcpyAsync(slab, pin, c->k * stride, hipMemcpyHostToDevice, c->stream));
+    int st = encode_rows(c, slab, len, plain_rows(stride), c->n * stride, 1, c->stream);
     if (st) return st;
-    for (size_t r = c->k; r < c->n; ++r)
-        HB_HIP(hipMemcpyAsync(shards[r], slab + r * stride, len, hipMemcpyDeviceToHost, c->stream));
+    HB_HIP(hipMemcpyAsync(pin + c->k * stride, slab + c->k * stride, c->m * stride,
+                          hipMemcpyDeviceToHost, c->stream));
     HB_HIP(hipStreamSynchronize(c->stream));
+    for (size_t r = c->k; r < c->n; ++r) std::memcpy(shards[r], pin + r * stride, len);
     return HBRBC_OK;
 }
 
@@ -927,30 +1363,33 @@ int hbrbc_reconstruct(hbrbc_ctx *c, uint8_t *const *shards, const size_t *lens,
     std::lock_guard<std::mutex> lk(c->shim_mu);
     HB_HIP(hipSetDevice(c->device));
     const size_t stride = round_up(len, 16);
-    HB_HIP(c->st_slab.ensure(c->n * stride));
-    HB_HIP(c->st_present.ensure(c->n));
-    HB_HIP(c->st_status.ensure(sizeof(int32_t)));
-    uint8_t *slab = c->st_slab.as<uint8_t>();
-    std::vector<uint8_t> pres(c->n);
+    const size_t pres_off = c->n * stride, stat_off = round_up(pres_off + c->n, 16);
+    HB_HIP(c->st_slab.ensure(stat_off + 16));
+    HB_HIP(c->pin.ensure(stat_off + 16));
+    uint8_t *slab = c->st_slab.as<uint8_t>(), *pin = c->pin.as<uint8_t>();
     for (size_t i = 0; i < c->n; ++i) {
-        pres[i] = present[i] ? 1 : 0;
-        if (pres[i])
-            HB_HIP(hipMemcpyAsync(slab + i * stride, shards[i], len, hipMemcpyHostToDevice,
-                                  c->stream));
+        pin[pres_off + i] = present[i] ? 1 : 0;
+        if (present[i]) std::memcpy(pin + i * stride, shards[i], len);
+        else std::memset(pin + i * stride, 0, len);
+        std::memset(pin + i * stride + len, 0, stride - len);
     }
-    HB_HIP(hipMemcpyAsync(c->st_present.p, pres.data(), c->n, hipMemcpyHostToDevice, c->stream));
-    int st = run_reconstruct(c, slab, len, stride, c->n * stride, c->st_present.as<uint8_t>(), 1,
-                             c->st_status.as<int32_t>(), c->stream);
+    HB_HIP(hipMemcpyAsync(slab, pin, pres_off + c->n, hipMemcpyHostToDevice, c->stream));
+    int32_t *dstat = reinterpret_cast<int32_t *>(slab + stat_off);
+    int st = run_reconstruct(c, slab, len, plain_rows(stride), c->n * stride, slab + pres_off, 1,
+                             dstat, c->stream);
     if (st) return st;
-    int32_t status = 0;
-    HB_HIP(hipMemcpyAsync(&status, c->st_status.p, sizeof status, hipMemcpyDeviceToHost,
+    HB_HIP(hipMemcpyAsync(pin + stat_off, dstat, sizeof(int32_t), hipMemcpyDeviceToHost,
                           c->stream));
     for (size_t i = 0; i < c->n; ++i)
-        if (!pres[i])
-            HB_HIP(hipMemcpyAsync(shards[i], slab + i * stride, len, hipMemcpyDeviceToHost,
+        if (!present[i])
+            HB_HIP(hipMemcpyAsync(pin + i * stride, slab + i * stride, len, hipMemcpyDeviceToHost,
                                   c->stream));
     HB_HIP(hipStreamSynchronize(c->stream));
+    int32_t status = 0;
+    std::memcpy(&status, pin + stat_off, sizeof status);
     if (status) return fail(status, "reconstruct status %d", status);
+    for (size_t i = 0; i < c->n; ++i)
+        if (!present[i]) std::memcpy(shards[i], pin + i * stride, len);
     return HBRBC_OK;
 }
 
@@ -963,32 +1402,35 @@ int hbrbc_merkle_build(const uint8_t *const *values, const size_t *lens, size_t 
     if (st) return st;
     std::lock_guard<std::mutex> lk(c->shim_mu);
     HB_HIP(hipSetDevice(c->device));
-    std::vector<uint64_t> offs(n);
-    std::vector<uint32_t> ls(n);
+    // pinned image: [offsets n x u64][lens n x u32][pad][values, 8-aligned]
+    const size_t lens_off = n * sizeof(uint64_t), vals_off = round_up(lens_off + n * 4, 16);
     size_t total = 0;
     for (size_t i = 0; i < n; ++i) {
         if (lens[i] > 0xFFFFFFFFull) return fail(HBRBC_E_INVALID_ARG, "value too long");
-        offs[i] = total;
-        ls[i] = (uint32_t)lens[i];
         total += round_up(lens[i], 8);
     }
-    std::vector<uint8_t> packed(total + 16, 0);
-    for (size_t i = 0; i < n; ++i)
-        if (lens[i]) std::memcpy(packed.data() + offs[i], values[i], lens[i]);
+    const size_t bytes = vals_off + total + 16;
     const size_t nodes = hbrbc_merkle_node_count(n);
-    HB_HIP(c->st_slab.ensure(packed.size()));
-    HB_HIP(c->st_aux.ensure(n * sizeof(uint64_t)));
-    HB_HIP(c->st_aux2.ensure(n * sizeof(uint32_t)));
+    HB_HIP(c->pin.ensure(std::max(bytes, nodes * 32)));
+    HB_HIP(c->st_slab.ensure(bytes));
     HB_HIP(c->st_nodes.ensure(nodes * 32));
-    HB_HIP(hipMemcpyAsync(c->st_slab.p, packed.data(), packed.size(), hipMemcpyHostToDevice,
-                          c->stream));
-    HB_HIP(hipMemcpyAsync(c->st_aux.p, offs.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice,
-                          c->stream));
-    HB_HIP(hipMemcpyAsync(c->st_aux2.p, ls.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          c->stream));
+    uint8_t *pin = c->pin.as<uint8_t>();
+    uint64_t *offs = reinterpret_cast<uint64_t *>(pin);
+    uint32_t *ls = reinterpret_cast<uint32_t *>(pin + lens_off);
+    size_t at = 0;
+    for (size_t i = 0; i < n; ++i) {
+        offs[i] = vals_off + at;
+        ls[i] = (uint32_t)lens[i];
+        if (lens[i]) std::memcpy(pin + vals_off + at, values[i], lens[i]);
+        std::memset(pin + vals_off + at + lens[i], 0, round_up(lens[i], 8) - lens[i]);
+        at += round_up(lens[i], 8);
+    }
+    std::memset(pin + vals_off + at, 0, 16);
+    uint8_t *dv = c->st_slab.as<uint8_t>();
+    HB_HIP(hipMemcpyAsync(dv, pin, bytes, hipMemcpyHostToDevice, c->stream));
     uint8_t *dn = c->st_nodes.as<uint8_t>();
-    HB_HIP(launch_ragged_hash(c->st_slab.as<uint8_t>(), c->st_aux.as<uint64_t>(),
-                              c->st_aux2.as<uint32_t>(), n, dn, c->stream));
+    HB_HIP(launch_ragged_hash(dv, reinterpret_cast<const uint64_t *>(dv),
+                              reinterpret_cast<const uint32_t *>(dv + lens_off), n, dn, c->stream));
     size_t off = 0, sz = n;
     while (sz > 1) {
         const size_t nsz = (sz + 1) / 2;
@@ -996,8 +1438,9 @@ int hbrbc_merkle_build(const uint8_t *const *values, const size_t *lens, size_t 
         off += sz;
         sz = nsz;
     }
-    HB_HIP(hipMemcpyAsync(nodes_out, dn, nodes * 32, hipMemcpyDeviceToHost, c->stream));
+    HB_HIP(hipMemcpyAsync(pin, dn, nodes * 32, hipMemcpyDeviceToHost, c->stream));
     HB_HIP(hipStreamSynchronize(c->stream));
+    std::memcpy(nodes_out, pin, nodes * 32);
     return HBRBC_OK;
 }
 
@@ -1036,43 +1479,47 @@ int hbrbc_proof_validate(const uint8_t *value, size_t len, size_t index, const u
     if (st) return st;
     std::lock_guard<std::mutex> lk(c->shim_mu);
     HB_HIP(hipSetDevice(c->device));
-    const size_t vbytes = round_up(len, 8) + 16;
+    // pinned image: [root 32][digests (dslots+1) x 32][meta 16][value, 8-aligned, +16]
     const size_t slots = dslots + 1;
-    HB_HIP(c->st_slab.ensure(vbytes));
-    HB_HIP(c->st_nodes.ensure(32 * slots + 32));
-    HB_HIP(c->st_aux.ensure(16));
-    HB_HIP(c->st_aux3.ensure(16));
-    std::vector<uint8_t> v(vbytes, 0), d(32 * slots + 32, 0);
-    if (len) std::memcpy(v.data(), value, len);
-    std::memcpy(d.data(), root, 32);
-    if (nd_dev) std::memcpy(d.data() + 32, digests, 32 * std::min(nd_dev, ndig));
-    uint8_t meta[16] = {0};
-    meta[0] = (uint8_t)nd_dev;
-    uint32_t idx = (uint32_t)index;
-    std::memcpy(meta + 4, &idx, 4);
-    HB_HIP(hipMemcpyAsync(c->st_slab.p, v.data(), vbytes, hipMemcpyHostToDevice, c->stream));
-    HB_HIP(hipMemcpyAsync(c->st_nodes.p, d.data(), d.size(), hipMemcpyHostToDevice, c->stream));
-    HB_HIP(hipMemcpyAsync(c->st_aux.p, meta, 16, hipMemcpyHostToDevice, c->stream));
+    const size_t dig_off = 32, meta_off = dig_off + 32 * slots, val_off = meta_off + 16;
+    const size_t bytes = val_off + round_up(len, 8) + 16;
+    HB_HIP(c->pin.ensure(bytes));
+    HB_HIP(c->st_slab.ensure(bytes + 16));
+    uint8_t *pin = c->pin.as<uint8_t>();
+    std::memset(pin, 0, val_off);
+    std::memcpy(pin, root, 32);
+    if (nd_dev) std::memcpy(pin + dig_off, digests, 32 * std::min(nd_dev, ndig));
+    pin[meta_off] = (uint8_t)nd_dev;
+    const uint32_t idx = (uint32_t)index;
+    std::memcpy(pin + meta_off + 4, &idx, 4);
+    if (len) std::memcpy(pin + val_off, value, len);
+    std::memset(pin + val_off + len, 0, bytes - val_off - len);
+    uint8_t *d = c->st_slab.as<uint8_t>();
+    HB_HIP(hipMemcpyAsync(d, pin, bytes, hipMemcpyHostToDevice, c->stream));
     ValidateArgs a;
-    a.values = c->st_slab.as<uint8_t>();
+    a.values = d + val_off;
     a.value_len = len;
-    a.value_stride = 0;
     a.value_inst_stride = 0;
     a.per_inst = 1;
-    a.indices = reinterpret_cast<const uint32_t *>(c->st_aux.as<uint8_t>() + 4);
-    a.digests = c->st_nodes.as<uint8_t>() + 32;
+    a.vrows = plain_rows(0);
+    a.rows = nullptr;
+    a.indices = reinterpret_cast<const uint32_t *>(d + meta_off + 4);
+    a.digests = d + dig_off;
     a.dslots = slots;
-    a.ndig = c->st_aux.as<uint8_t>();
-    a.roots = c->st_nodes.as<uint8_t>();
+    a.dig_rows = 1;
+    a.ndig = d + meta_off;
+    a.roots = d;
     a.root_stride = 0;
     a.tree_n = n;
     a.count = 1;
-    a.ok_out = c->st_aux3.as<uint8_t>();
+    a.ok_out = d + meta_off + 8;
+    a.leaf_out = nullptr;
+    a.leaf_inst_stride = 0;
     HB_HIP(launch_validate(a, c->stream));
-    uint8_t ok = 0;
-    HB_HIP(hipMemcpyAsync(&ok, a.ok_out, 1, hipMemcpyDeviceToHost, c->stream));
+    HB_HIP(hipMemcpyAsync(pin + meta_off + 8, d + meta_off + 8, 1, hipMemcpyDeviceToHost,
+                          c->stream));
     HB_HIP(hipStreamSynchronize(c->stream));
-    *valid_out = ok ? 1 : 0;
+    *valid_out = pin[meta_off + 8] ? 1 : 0;
     return HBRBC_OK;
 }
 
@@ -1155,52 +1602,83 @@ int hbrbc_wire_decode_batch(hbrbc_ctx *c, const uint8_t *msgs, size_t msg_stride
     return HBRBC_OK;
 }
 
+
 // ------------------------------------------------------ specialised encode --
 const char *hbrbc_encode_kernel(const hbrbc_ctx *c) { return c ? c->enc_kind.c_str() : "none"; }
 
 size_t hbrbc_jit_encode_groups(size_t data_shards, size_t parity_shards) {
     if (data_shards == 0 || parity_shards == 0) return 0;
-    return encode_groups(data_shards, parity_shards, spec_row_tile(data_shards, parity_shards))
-        .size();
+    return xor_groups(data_shards, parity_shards, spec_row_tile(data_shards, parity_shards)).size();
+}
+
+int hbrbc_jit_build_encode_rows(size_t data_shards, size_t parity_shards, size_t group,
+                                size_t rows_per_block, const char *dir) {
+    if (data_shards == 0 || parity_shards == 0 || data_shards + parity_shards > 256)
+        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, data + parity <= 256");
+    const size_t n = data_shards + parity_shards;
+    std::vector<uint8_t> mat;
+    if (!build_matrix(data_shards, n, mat))
+        return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
+    const int rt = spec_row_tile(data_shards, parity_shards), depth = spec_depth();
+    const int rb = (rows_per_block && rows_per_block < n) ? (int)rows_per_block : 256;
+    const auto groups = xor_groups(data_shards, parity_shards, rt);
+    if (group >= groups.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group,
+                                            groups.size());
+    const XorProgram p = encode_program(data_shards, parity_shards,
+                                        mat.data() + data_shards * data_shards, rt, depth,
+                                        groups[group].first, groups[group].second, rb);
+    std::vector<char> code;
+    std::string log;
+    if (compile_source(gen_xor_source(p), code, log))
+        return fail(HBRBC_E_DEVICE, "hiprtc: %s", log.substr(0, 400).c_str());
+    const std::string d = dir ? std::string(dir) : jit_dir();
+    mkdir(d.c_str(), 0755);
+    const std::string path = jit_file(d, p.name);
+    return write_file(path, code) ? HBRBC_OK
+                                  : fail(HBRBC_E_INVALID_ARG, "cannot write %s", path.c_str());
 }
 
 int hbrbc_jit_build_encode_group(size_t data_shards, size_t parity_shards, size_t group,
                                  const char *dir) {
-    if (data_shards == 0 || parity_shards == 0 || data_shards + parity_shards > 256)
-        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, data + parity <= 256");
-    std::vector<uint8_t> mat;
-    if (!build_matrix(data_shards, data_shards + parity_shards, mat))
-        return fail(HBRBC_E_SINGULAR_MATRIX, "singular Vandermonde top block");
-    const int rt = spec_row_tile(data_shards, parity_shards), depth = spec_depth();
-    const auto groups = encode_groups(data_shards, parity_shards, rt);
+    return hbrbc_jit_build_encode_rows(data_shards, parity_shards, group, 0, dir);
+}
+
+int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t group,
+                               size_t rows_per_block, char *buf, size_t buf_len) {
+    if (data_shards == 0 || parity_shards == 0 || !buf)
+        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, a buffer");
+    const size_t n = data_shards + parity_shards;
+    const int rt = spec_row_tile(data_shards, parity_shards);
+    const int rb = (rows_per_block && rows_per_block < n) ? (int)rows_per_block : 256;
+    const auto groups = xor_groups(data_shards, parity_shards, rt);
     if (group >= groups.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group,
                                             groups.size());
-    std::vector<char> code;
-    std::string log;
-    if (compile_encode(data_shards, parity_shards, mat.data() + data_shards * data_shards, rt,
-                       depth, groups[group].first, groups[group].second, code, log))
-        return fail(HBRBC_E_DEVICE, "hiprtc: %s", log.substr(0, 400).c_str());
-    const std::string d = dir ? std::string(dir) : jit_dir();
-    mkdir(d.c_str(), 0755);
-    const std::string path =
-        jit_file(d, data_shards, parity_shards, rt, depth, groups[group].first);
-    FILE *f = fopen(path.c_str(), "wb");
-    if (!f) return fail(HBRBC_E_INVALID_ARG, "cannot write %s", path.c_str());
-    const bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
-    fclose(f);
-    return ok ? HBRBC_OK : fail(HBRBC_E_INVALID_ARG, "short write %s", path.c_str());
+    const std::string f =
+        jit_file("", encode_kernel_name(data_shards, parity_shards, rt, spec_depth(),
+                                        groups[group].first, rb)).substr(1);
+    if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
+    std::memcpy(buf, f.c_str(), f.size() + 1);
+    return HBRBC_OK;
 }
 
 int hbrbc_jit_file_name(size_t data_shards, size_t parity_shards, size_t group, char *buf,
                         size_t buf_len) {
-    if (data_shards == 0 || parity_shards == 0 || !buf)
-        return fail(HBRBC_E_INVALID_ARG, "need data >= 1, parity >= 1, a buffer");
-    const int rt = spec_row_tile(data_shards, parity_shards);
-    const auto groups = encode_groups(data_shards, parity_shards, rt);
-    if (group >= groups.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group,
-                                            groups.size());
-    const std::string f = jit_file("", data_shards, parity_shards, rt, spec_depth(),
-                                   groups[group].first).substr(1);
+    return hbrbc_jit_encode_file_name(data_shards, parity_shards, group, 0, buf, buf_len);
+}
+
+int hbrbc_jit_decode_file_name(size_t data_shards, size_t parity_shards, const uint8_t *present,
+                               size_t rows_per_block, size_t group, char *buf, size_t buf_len) {
+    std::vector<uint8_t> mat;
+    const size_t n = data_shards + parity_shards;
+    if (!present || !buf || data_shards == 0 || n > 256 || !build_matrix(data_shards, n, mat))
+        return fail(HBRBC_E_INVALID_ARG, "bad arguments");
+    const int rb = (rows_per_block && rows_per_block < n) ? (int)rows_per_block : 256;
+    std::vector<XorProgram> progs;
+    uint64_t hash;
+    int rt;
+    if (!decode_programs(mat, data_shards, n, present, rb, progs, hash, rt) || group >= progs.size())
+        return fail(HBRBC_E_INVALID_ARG, "no such decoder group");
+    const std::string f = jit_file("", progs[group].name).substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
     std::memcpy(buf, f.c_str(), f.size() + 1);
     return HBRBC_OK;
@@ -1226,9 +1704,6 @@ int hbrbc_profile_enable(hbrbc_ctx *c, int enable) {
 int hbrbc_profile_reset(hbrbc_ctx *c) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
     HB_HIP(hipSetDevice(c->device));
-    for (auto &r : c->recs) {
-        (void)r;
-    }
     c->recs.clear();
     c->ev_used = 0;
     return HBRBC_OK;

@@ -1,36 +1,42 @@
-// jit.hip -- specialised Reed-Solomon encode kernels, generated per encoding
+// jit.hip -- matrix-specialised GF(2^8) kernels, generated per coefficient
 // matrix and compiled with hiprtc for gfx950.
 //
 // Why: Coding::encode (broadcast.rs:193 -> rse encode) multiplies the k data
-// rows by the fixed m x k parity block of rse `build_matrix(k, n)`.  The
-// generic bit-sliced kernel (kernels.hip, gf_bitslice_kernel) reads every
-// coefficient at run time and pays a wave-uniform branch per coefficient bit
-// plus the doubling chain.  With the matrix known when the `Coding` context
-// is built (like `ReedSolomon::new`), each product c * x becomes a fixed XOR
-// network on the 8 bit planes of x: output plane q of c*x is the XOR of the
-// input planes p with bit q of c*2^p set.  The generated kernel is that
-// network written out for every (parity row, data row), accumulated with
-// three-input XORs (v_bitop3): about 2.25 VALU per plane per coefficient
-// against ~4 XORs + branches in the generic kernel, and no branches at all.
-// Passes of at most 8 rows use a nibble-subset network instead (one VALU per
-// plane per coefficient, gen_nibble_network); at 14-row passes its longer
-// live ranges cost occupancy and it measured slower (5.7 -> 9.0 ms, cfg3).
+// rows by the fixed m x k parity block of rse `build_matrix(k, n)`, and a
+// reconstruct of one erasure pattern (broadcast.rs:569 -> rse reconstruct,
+// whose decode matrix rse caches per pattern) multiplies the first k present
+// rows by a fixed recovery matrix.  The generic bit-sliced kernel (kernels.hip,
+// gf_bitslice_kernel) reads every coefficient at run time and pays a
+// wave-uniform branch per coefficient bit plus the doubling chain.  With the
+// matrix known in advance each product c * x becomes a fixed XOR network on
+// the 8 bit planes of x: output plane q of c*x is the XOR of the input planes
+// p with bit q of c*2^p set.  The generated kernel is that network written
+// out for every (output row, input row), accumulated with three-input XORs
+// (v_bitop3): about 2.25 VALU per plane per coefficient against ~4 XORs +
+// branches in the generic kernel, and no branches at all.  Passes of at most
+// 8 rows use a nibble-subset network instead (one VALU per plane per
+// coefficient, gen_nibble_network); at 14-row passes its longer live ranges
+// cost occupancy and it measured slower (5.7 -> 9.0 ms, cfg3).
 //
 // Layout and lane mapping are those of gf_bitslice_kernel: a lane owns 32
 // consecutive byte positions of every row; a workgroup holds up to 4 waves
-// over the same positions, wave w producing passes w, w+4, ... of RT parity
-// rows.  Output is bit-identical to the generic kernels (tests compare both
-// with the oracle).
+// over the same positions, wave w producing passes w, w+4, ... of rt output
+// rows.  Rows are addressed through one buffer resource per row block (the
+// blocked layouts of the validator-sharded simulation, launchers.hpp RowMap)
+// and an SGPR row offset.  Output is bit-identical to the generic kernel
+// (tests compare both with the oracle).
 //
-// Code objects are cached as files (<lib dir>/jit/enc_k<k>_m<m>_rt<rt>_d<depth>_r<first row>_v10.co);
-// __graft_entry__.build() pre-generates them for the BASELINE validator
-// counts, and a context loads the file when present.  Compiling a missing
-// one at context creation is opt-in (HBRBC_JIT=1) since it takes seconds.
+// Code objects are cached as files under <lib dir>/jit (names from
+// encode_kernel_name / decode_kernel_name + "_v11.co");
+// __graft_entry__.build() pre-generates the encoders of the BASELINE
+// validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -101,20 +107,26 @@ __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
 }
 )";
 
-// Nibble-subset XOR network of data row j for parity rows r0..r0+rows-1:
+// coefficient of (output t, input jj)
+struct CoefView {
+    const uint8_t *c;
+    size_t nin;
+    uint8_t at(int t, size_t jj) const { return c[(size_t)t * nin + jj]; }
+};
+
+// Nibble-subset XOR network of input jj for output rows t0..t0+rows-1:
 // output plane q of c*x is the XOR of a low-nibble subset (planes 0-3) and a
 // high-nibble subset (planes 4-7) of the input planes.  The subset XORs used
-// by this data row are built once (<= 11 + 11 ops) and shared by every row of
+// by this input are built once (<= 11 + 11 ops) and shared by every row of
 // the pass; each accumulator then takes exactly one op.  Fewer VALU than the
 // pairwise network but more values live across the row, so it is used for
 // short passes only (rt <= 8, the split N = 250 programs: encode 16.9 ->
 // 15.0 ms per 1024 instances; at rt 14 it costs 2 waves/SIMD of occupancy).
-void gen_nibble_network(std::ostringstream &o, size_t k, const uint8_t *parity_rows, int r0,
-                        int rows, size_t j) {
+void gen_nibble_network(std::ostringstream &o, const CoefView &cv, int t0, int rows, size_t jj) {
     std::vector<std::pair<int, int>> tgt((size_t)rows * 8, {0, 0});
     bool used[2][16] = {};
     for (int t = 0; t < rows; ++t) {
-        const uint8_t c = parity_rows[(size_t)(r0 + t) * k + j];
+        const uint8_t c = cv.at(t0 + t, jj);
         if (!c) continue;
         uint8_t col[8];
         for (int q = 0; q < 8; ++q) col[q] = gf_mul_host(c, (uint8_t)(1u << q));
@@ -163,55 +175,100 @@ void gen_nibble_network(std::ostringstream &o, size_t k, const uint8_t *parity_r
         }
 }
 
-}  // namespace
-
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, bool fused, int r_lo) {
-    char b[112];
-    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d%s", k, m, rt, depth, r_lo,
-             fused ? "_fe" : "");
-    return b;
+// Pairwise network: term lists of every (row, plane); output plane q of c*x
+// is the XOR of the planes p with bit q of c*2^p set.  Terms are paired in
+// order ((p1,p2), (p3,p4), ...); the pair XORs are computed once per input
+// and shared by all rows of the pass, and each v_bitop3 folds two pairs --
+// up to four planes -- into an accumulator.
+void gen_pair_network(std::ostringstream &o, const CoefView &cv, int t0, int rows, size_t jj) {
+    std::vector<std::vector<int>> elems((size_t)rows * 8);
+    bool used[8][8] = {};
+    for (int t = 0; t < rows; ++t) {
+        const uint8_t c = cv.at(t0 + t, jj);
+        if (!c) continue;
+        uint8_t col[8];
+        for (int q = 0; q < 8; ++q) col[q] = gf_mul_host(c, (uint8_t)(1u << q));
+        for (int q = 0; q < 8; ++q) {
+            std::vector<int> terms;
+            for (int pp = 0; pp < 8; ++pp)
+                if ((col[pp] >> q) & 1) terms.push_back(pp);
+            auto &el = elems[(size_t)t * 8 + q];
+            for (size_t i = 0; i + 1 < terms.size(); i += 2) {
+                used[terms[i]][terms[i + 1]] = true;
+                el.push_back(8 + terms[i] * 8 + terms[i + 1]);  // pair id
+            }
+            if (terms.size() & 1) el.push_back(terms.back());   // single plane
+        }
+    }
+    for (int a = 0; a < 8; ++a)
+        for (int b = a + 1; b < 8; ++b)
+            if (used[a][b])
+                o << "        const uint32_t p" << a << b << " = x[" << a << "] ^ x[" << b << "];\n";
+    auto name = [](int e) {
+        return e < 8 ? "x[" + std::to_string(e) + "]"
+                     : "p" + std::to_string((e - 8) / 8) + std::to_string((e - 8) % 8);
+    };
+    for (int t = 0; t < rows; ++t)
+        for (int q = 0; q < 8; ++q) {
+            const auto &el = elems[(size_t)t * 8 + q];
+            const std::string acc = "a[" + std::to_string(t) + "][" + std::to_string(q) + "]";
+            size_t i = 0;
+            for (; i + 1 < el.size(); i += 2)
+                o << "        " << acc << " = __builtin_amdgcn_bitop3_b32(" << acc << ", "
+                  << name(el[i]) << ", " << name(el[i + 1]) << ", 0x96);\n";
+            if (i < el.size()) o << "        " << acc << " ^= " << name(el[i]) << ";\n";
+        }
 }
 
-std::vector<std::pair<int, int>> encode_groups(size_t k, size_t m, int rt) {
-    // a group = one hiprtc program; bigger ones compile superlinearly slowly
-    const size_t kMaxCoefs = 4096;
-    std::vector<std::pair<int, int>> g;
-    size_t per = m;
-    if (k * m > kMaxCoefs) per = std::max<size_t>((size_t)rt, kMaxCoefs / k / rt * rt);
-    for (size_t lo = 0; lo < m; lo += per) g.push_back({(int)lo, (int)std::min(m, lo + per)});
-    return g;
-}
-
-std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
-                              bool fused, int r_lo, int r_hi) {
-    (void)m;
-    const int npass = (r_hi - r_lo + rt - 1) / rt;
-    if (fused) depth = fused_depth(depth);  // 36 bytes per row in flight
+// One kernel of a program: `fused` = the frame+encode twin.
+std::string gen_xor_kernel(const XorProgram &p, bool fused) {
+    const size_t nin = p.in_rows.size();
+    const int nout = (int)p.out_rows.size();
+    const int rt = p.rt;
+    const int npass = (nout + rt - 1) / rt;
+    const int depth = fused ? std::min(p.depth, 2) : p.depth;  // 36 bytes per row in flight when fused
     const int nbuf = depth + 1;
+    const int rb = p.rb;
+    const CoefView cv{p.coefs.data(), nin};
+    auto blk = [&](int row) { return row / rb; };
+    auto rin = [&](int row) { return row % rb; };
+    std::set<int> blocks;
+    for (int r : p.in_rows) blocks.insert(blk(r));
+    for (int r : p.out_rows) blocks.insert(blk(r));
     std::ostringstream o;
-    o << "\nextern \"C\" __global__ __launch_bounds__(256) void "
-      << encode_kernel_name(k, m, rt, depth, fused, r_lo)
+    o << "\nextern \"C\" __global__ __launch_bounds__(256) void " << p.name << (fused ? "_fe" : "")
       << "(uint8_t *__restrict__ base, unsigned long inst_stride, unsigned long shard_stride,\n"
-         "    unsigned row_bytes, unsigned waves_per_row"
-      << (fused ? ", const uint8_t *__restrict__ payloads, unsigned long payload_stride,\n"
-                  "    unsigned P, unsigned S" : "")
-      << ", int p_only) {\n"
-         "  const unsigned long inst = blockIdx.x / waves_per_row;\n"
-         "  const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);\n"
+         "    unsigned long block_stride, unsigned row_bytes, unsigned waves_per_row,\n"
+         "    const uint8_t *__restrict__ payloads, unsigned long payload_stride, unsigned P, unsigned S,\n"
+         "    const int *__restrict__ pat, const unsigned long *__restrict__ slot_hash, int hash_slots,\n"
+         "    int p_only) {\n"
+         "  const unsigned long inst = blockIdx.x / waves_per_row;\n";
+    if (p.guard) {
+        // reconstruct of one cached erasure pattern: other patterns return
+        char g[64];
+        snprintf(g, sizeof g, "0x%016llxull", (unsigned long long)p.guard);
+        o << "  { const int sl_ = pat[inst];\n"
+             "    if (sl_ >= hash_slots || slot_hash[sl_] != "
+          << g << ") return; }\n";
+    }
+    o << "  const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);\n"
          "  const unsigned chunk = (blockIdx.x - (unsigned)inst * waves_per_row) * 64u + (threadIdx.x & 63u);\n"
          "  unsigned off = chunk * 32u;\n"
          "  const bool active = off < row_bytes;\n"
          "  if (!active) off = row_bytes - 16u;\n"
          "  const bool full = off + 32u <= row_bytes;\n"
          "  const unsigned off2 = full ? off + 16u : off;\n"
-         // raw buffer ops: the instance base lives in a scalar resource, the
-         // row offset j * shard_stride in an SGPR (soffset) and the lane
-         // offset in one VGPR -- no per-lane 64-bit address per row
-         "  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(\n"
-         "      base + inst * inst_stride, (short)0, 0x7fffffff, 0x00020000);\n"
-         "  const unsigned sst = (unsigned)shard_stride;\n"
-         "#define HB_LD(L, H, j) { L = __builtin_amdgcn_raw_buffer_load_b128(rs, off, (j) * sst, 0); "
-         "H = __builtin_amdgcn_raw_buffer_load_b128(rs, off2, (j) * sst, 0); }\n";
+         // raw buffer ops: each row block's base lives in a scalar resource,
+         // the row offset (row % rb) * shard_stride in an SGPR (soffset) and
+         // the lane offset in one VGPR -- no per-lane 64-bit address per row
+         "  uint8_t *const ib = base + inst * inst_stride;\n";
+    for (int q : blocks)
+        o << "  const __amdgpu_buffer_rsrc_t rs" << q << " = __builtin_amdgcn_make_buffer_rsrc(ib"
+          << (q ? " + " + std::to_string(q) + "ul * block_stride" : std::string()) << ", (short)0, "
+          << "0x7fffffff, 0x00020000);\n";
+    o << "  const unsigned sst = (unsigned)shard_stride;\n"
+         "#define HB_LD(L, H, Q, R) { L = __builtin_amdgcn_raw_buffer_load_b128(rs##Q, off, (R) * sst, 0); "
+         "H = __builtin_amdgcn_raw_buffer_load_b128(rs##Q, off2, (R) * sst, 0); }\n";
     if (fused)
         // framing (broadcast.rs:174-189) folded into the loads: logical byte b
         // of the framed value is payload byte b - 4.  The buffer resource
@@ -239,56 +296,57 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
          "  const int p_hi = p_only >= 0 ? p_only + 1 : " << npass << ";\n"
          "  const int p_st = p_only >= 0 ? 1 : nw;\n"
          "  for (int p = p_lo; p < p_hi; p += p_st) {\n    switch (p) {\n";
-    for (int p = 0; p < npass; ++p) {
-        const int r0 = r_lo + p * rt;
-        const int rows = std::min(rt, r_hi - r0);
+    for (int ps = 0; ps < npass; ++ps) {
+        const int t0 = ps * rt;
+        const int rows = std::min(rt, nout - t0);
         // a distinct barrier opens every case, so no common prefix (the first
         // rows' loads) is hoisted above the switch and kept live across it
-        o << "    case " << p << ": {\n      __asm__ volatile(\"; pass " << p
+        o << "    case " << ps << ": {\n      __asm__ volatile(\"; pass " << ps
           << "\" ::: \"memory\");\n      uint32_t a[" << rows << "][8] = {};\n";
         if (fused)
             o << "      u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "];\n";
         else
             o << "      u32x4 l[" << nbuf << "], h[" << nbuf << "];\n";
-        auto load = [&](size_t j) {
-            const int b = (int)(j % nbuf);
+        auto load = [&](size_t jj) {
+            const int b = (int)(jj % nbuf);
+            const int row = p.in_rows[jj];
             if (fused)
-                o << "      HB_LDF(q0[" << b << "], q1[" << b << "], q2[" << b << "], " << j << "u)";
+                o << "      HB_LDF(q0[" << b << "], q1[" << b << "], q2[" << b << "], " << row << "u)";
             else
-                o << "      HB_LD(l[" << b << "], h[" << b << "], " << j << ")";
+                o << "      HB_LD(l[" << b << "], h[" << b << "], " << blk(row) << ", " << rin(row) << "u)";
             // the empty asm keeps the scheduler from hoisting every row's load to
             // the top of the straight-line pass (hundreds of live VGPRs)
             o << " __asm__ volatile(\"\" ::: \"memory\");\n";
         };
-        // rows 0..depth-1 in flight before the first product; row j + depth is
-        // requested while row j is consumed (depth rows of HBM latency hidden)
-        for (int j = 0; j < depth && j < (int)k; ++j) load((size_t)j);
-        for (size_t j = 0; j < k; ++j) {
-            const int cur = (int)(j % nbuf);
-            if (j + depth < k) load(j + depth);
+        // inputs 0..depth-1 in flight before the first product; input jj + depth
+        // is requested while input jj is consumed (depth rows of HBM latency hidden)
+        for (int jj = 0; jj < depth && jj < (int)nin; ++jj) load((size_t)jj);
+        for (size_t jj = 0; jj < nin; ++jj) {
+            const int cur = (int)(jj % nbuf);
+            const int row = p.in_rows[jj];
+            if (jj + depth < nin) load(jj + depth);
             if (fused) {
                 const std::string c = std::to_string(cur);
                 o << "      { uint32_t x[8];\n"
-                  << "        hb_window(q0[" << c << "], q1[" << c << "], q2[" << c << "], (" << j
+                  << "        hb_window(q0[" << c << "], q1[" << c << "], q2[" << c << "], (" << row
                   << "u * S - 4u) & 3u, x);\n";
                 // windows touching the BE32 payload length (broadcast.rs:175-177);
                 // j * S < 4 needs j < 4 since S >= 1
-                if (j < 4)
-                    o << "        if (" << j << "u * S < 4u) { if (off == 0u) hb_frame_slow(payloads + inst * "
-                     "payload_stride, P, " << j << "u * S, x); }\n";
+                if (row < 4)
+                    o << "        if (" << row << "u * S < 4u) { if (off == 0u) hb_frame_slow(payloads + inst * "
+                     "payload_stride, P, " << row << "u * S, x); }\n";
                 // positions >= S of this row belong to the next shard: zero
                 o << "        if (edge) {\n"
                      "          _Pragma(\"unroll\") for (int i_ = 0; i_ < 8; ++i_) {\n"
                      "            const int lim_ = (int)S - (int)off - 4 * i_;\n"
                      "            x[i_] = lim_ >= 4 ? x[i_] : (lim_ <= 0 ? 0u : x[i_] & (0xFFFFFFFFu >> (8 * (4 - lim_))));\n"
                      "          }\n        }\n";
-                if (p == 0 && r_lo == 0)  // pass 0 of group 0 also writes the framed data row
+                if (ps == 0 && p.out_rows.front() == (int)nin)  // pass 0 of group 0 also writes the framed data row
                     o << "        if (active) {\n"
-                         "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[0], x[1], x[2], x[3]}, rs, off, "
-                      << j << "u * sst, HB_ST_AUX);\n"
+                         "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[0], x[1], x[2], x[3]}, rs"
+                      << blk(row) << ", off, " << rin(row) << "u * sst, HB_ST_AUX);\n"
                          "          if (full) __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[4], x[5], x[6], x[7]}, "
-                         "rs, off2, "
-                      << j << "u * sst, HB_ST_AUX);\n        }\n";
+                         "rs" << blk(row) << ", off2, " << rin(row) << "u * sst, HB_ST_AUX);\n        }\n";
                 o << "        hb_tr(x);\n";
             } else {
                 const std::string lc = "l[" + std::to_string(cur) + "]";
@@ -296,92 +354,75 @@ std::string gen_encode_kernel(size_t k, size_t m, const uint8_t *parity_rows, in
                   << "        uint32_t x[8] = {" << lc << "[0], " << lc << "[1], " << lc << "[2], " << lc
                   << "[3], hh[0], hh[1], hh[2], hh[3]};\n        hb_tr(x);\n";
             }
-            if (rt <= 8) {   // short passes: the nibble-subset network (below)
-                gen_nibble_network(o, k, parity_rows, r0, rows, j);
-                o << "        for (int t_ = 0; t_ < " << rows << "; ++t_) for (int q_ = 0; q_ < 8; ++q_) "
-                     "__asm__ volatile(\"\" : \"+v\"(a[t_][q_]));\n      }\n";
-                continue;
-            }
-            // Term lists of every (row, plane): output plane q of c*x is the
-            // XOR of the planes p with bit q of c*2^p set.  Terms are paired in
-            // order ((p1,p2), (p3,p4), ...); the pair XORs are computed once per
-            // data row and shared by all rows of the pass, and each v_bitop3
-            // folds two pairs -- up to four planes -- into an accumulator.
-            std::vector<std::vector<int>> elems((size_t)rows * 8);
-            bool used[8][8] = {};
-            for (int t = 0; t < rows; ++t) {
-                const uint8_t c = parity_rows[(size_t)(r0 + t) * k + j];
-                if (!c) continue;
-                uint8_t col[8];
-                for (int q = 0; q < 8; ++q) col[q] = gf_mul_host(c, (uint8_t)(1u << q));
-                for (int q = 0; q < 8; ++q) {
-                    std::vector<int> terms;
-                    for (int pp = 0; pp < 8; ++pp)
-                        if ((col[pp] >> q) & 1) terms.push_back(pp);
-                    auto &el = elems[(size_t)t * 8 + q];
-                    for (size_t i = 0; i + 1 < terms.size(); i += 2) {
-                        used[terms[i]][terms[i + 1]] = true;
-                        el.push_back(8 + terms[i] * 8 + terms[i + 1]);  // pair id
-                    }
-                    if (terms.size() & 1) el.push_back(terms.back());   // single plane
-                }
-            }
-            for (int a = 0; a < 8; ++a)
-                for (int b = a + 1; b < 8; ++b)
-                    if (used[a][b])
-                        o << "        const uint32_t p" << a << b << " = x[" << a << "] ^ x[" << b << "];\n";
-            auto name = [](int e) {
-                return e < 8 ? "x[" + std::to_string(e) + "]"
-                             : "p" + std::to_string((e - 8) / 8) + std::to_string((e - 8) % 8);
-            };
-            for (int t = 0; t < rows; ++t)
-                for (int q = 0; q < 8; ++q) {
-                    const auto &el = elems[(size_t)t * 8 + q];
-                    const std::string acc = "a[" + std::to_string(t) + "][" + std::to_string(q) + "]";
-                    size_t i = 0;
-                    for (; i + 1 < el.size(); i += 2)
-                        o << "        " << acc << " = __builtin_amdgcn_bitop3_b32(" << acc << ", "
-                          << name(el[i]) << ", " << name(el[i + 1]) << ", 0x96);\n";
-                    if (i < el.size()) o << "        " << acc << " ^= " << name(el[i]) << ";\n";
-                }
-            // pin the accumulators after every data row: without this the
+            if (rt <= 8)   // short passes: the nibble-subset network
+                gen_nibble_network(o, cv, t0, rows, jj);
+            else
+                gen_pair_network(o, cv, t0, rows, jj);
+            // pin the accumulators after every input: without this the
             // reassociation pass flattens each accumulator's whole XOR chain
-            // over all k rows and keeps every row's planes live at once
+            // over all inputs and keeps every input's planes live at once
             o << "        for (int t_ = 0; t_ < " << rows << "; ++t_) for (int q_ = 0; q_ < 8; ++q_) "
                  "__asm__ volatile(\"\" : \"+v\"(a[t_][q_]));\n      }\n";
         }
         o << "      if (active) {\n";
         for (int t = 0; t < rows; ++t) {
+            const int row = p.out_rows[t0 + t];
             const std::string at = "a[" + std::to_string(t) + "]";
-            o << "        { hb_tr(" << at << "); const unsigned so_ = " << k + r0 + t << "u * sst;\n"
+            o << "        { hb_tr(" << at << "); const unsigned so_ = " << rin(row) << "u * sst;\n"
               << "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){" << at << "[0], " << at << "[1], "
-              << at << "[2], " << at << "[3]}, rs, off, so_, HB_ST_AUX);\n"
+              << at << "[2], " << at << "[3]}, rs" << blk(row) << ", off, so_, HB_ST_AUX);\n"
               << "          if (full) __builtin_amdgcn_raw_buffer_store_b128((u32x4){" << at << "[4], " << at
-              << "[5], " << at << "[6], " << at << "[7]}, rs, off2, so_, HB_ST_AUX); }\n";
+              << "[5], " << at << "[6], " << at << "[7]}, rs" << blk(row) << ", off2, so_, HB_ST_AUX); }\n";
         }
         o << "      }\n      break; }\n";
     }
-    o << "    }\n  }\n}\n";
+    o << "    }\n  }\n}\n#undef HB_LD\n" << (fused ? "#undef HB_LDF\n" : "");
     return o.str();
 }
 
-std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
-                              int r_lo, int r_hi) {
-    return std::string(kPrelude) +
-           gen_encode_kernel(k, m, parity_rows, rt, depth, false, r_lo, r_hi) +
-           gen_encode_kernel(k, m, parity_rows, rt, depth, true, r_lo, r_hi);
+}  // namespace
+
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb) {
+    char b[128];
+    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d", k, m, rt, depth, r_lo);
+    std::string s = b;
+    if (rb < 256) s += "_b" + std::to_string(rb);
+    return s;
 }
 
-int compile_encode(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth, int r_lo,
-                   int r_hi, std::vector<char> &code, std::string &log) {
-    const std::string src = gen_encode_source(k, m, parity_rows, rt, depth, r_lo, r_hi);
+std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb) {
+    char b[128];
+    snprintf(b, sizeof b, "hbrbc_dec_n%zu_%016llx_rt%d_d%d_g%d", n, (unsigned long long)hash, rt,
+             depth, group);
+    std::string s = b;
+    if (rb < 256) s += "_b" + std::to_string(rb);
+    return s;
+}
+
+std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt) {
+    // a group = one hiprtc program; bigger ones compile superlinearly slowly
+    const size_t kMaxCoefs = 4096;
+    std::vector<std::pair<int, int>> g;
+    size_t per = nout;
+    if (nin * nout > kMaxCoefs) per = std::max<size_t>((size_t)rt, kMaxCoefs / nin / rt * rt);
+    for (size_t lo = 0; lo < nout; lo += per) g.push_back({(int)lo, (int)std::min(nout, lo + per)});
+    return g;
+}
+
+std::string gen_xor_source(const XorProgram &p) {
+    std::string s = std::string(kPrelude) + gen_xor_kernel(p, false);
+    if (p.fused) s += gen_xor_kernel(p, true);
+    return s;
+}
+
+int compile_source(const std::string &src, std::vector<char> &code, std::string &log) {
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "hbrbc_enc.hip", 0, nullptr, nullptr) !=
+    if (hiprtcCreateProgram(&prog, src.c_str(), "hbrbc_xor.hip", 0, nullptr, nullptr) !=
         HIPRTC_SUCCESS) {
         log = "hiprtcCreateProgram failed";
         return -1;
     }
-    // HBRBC_ST_AUX (A/B): cache-policy bits of the parity stores
+    // HBRBC_ST_AUX (A/B): cache-policy bits of the row stores
     const char *aux = getenv("HBRBC_ST_AUX");
     const std::string aux_def = std::string("-DHB_ST_AUX=") + (aux ? aux : "2");
     const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", aux_def.c_str()};

@@ -1,4 +1,4 @@
-// jit.hpp -- specialised RS encode kernels (see jit.hip).  Internal.
+// jit.hpp -- matrix-specialised GF(2^8) XOR-network kernels (see jit.hip).  Internal.
 #pragma once
 
 #include <stddef.h>
@@ -10,22 +10,49 @@
 
 namespace hbrbc {
 
-// Kernel symbol of the specialised encoder for parity rows [r_lo, ...) of
-// (k, m) with tile rt and prefetch depth; `fused` names its frame+encode twin
-// (which keeps min(depth, 2) rows in flight).
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, bool fused, int r_lo);
-// Parity-row groups [lo, hi), one hiprtc program each (large matrices are
+// One hiprtc program: out_row[t] = sum_jj coefs[t][jj] * in_row[jj] over
+// GF(2^8), every coefficient compiled into the code.
+//  * Coding::encode: in_rows = data rows 0..k-1, out_rows = a group of parity
+//    rows; `fused` adds the frame+encode twin NAME_fe that reads the payload
+//    instead of the data rows (broadcast.rs:174-193).
+//  * reconstruct of one cached erasure pattern: in_rows = the first k present
+//    rows, out_rows = (a group of) the missing rows, coefs = the decode rows;
+//    `guard` = the pattern's hash, so instances of other patterns return.
+// Row placement: row j at (j / rb) * block_stride + (j % rb) * shard_stride
+// past the instance base (rb >= 256: plain shard-major).
+struct XorProgram {
+    std::string name;
+    std::vector<int> in_rows, out_rows;
+    std::vector<uint8_t> coefs;  // [out_rows.size()][in_rows.size()]
+    int rt = 2, depth = 4, rb = 256;
+    uint64_t guard = 0;
+    bool fused = false;
+};
+
+// Kernel argument list shared by every generated kernel (hipModuleLaunchKernel).
+struct XorArgs {
+    uint8_t *base;
+    unsigned long inst_stride, shard_stride, block_stride;
+    unsigned row_bytes, waves_per_row;
+    const uint8_t *payloads;
+    unsigned long payload_stride;
+    unsigned P, S;
+    const int *pat;
+    const unsigned long *slot_hash;
+    int hash_slots;
+    int p_only;
+};
+
+std::string gen_xor_source(const XorProgram &p);
+// hiprtc-compile a generated source for gfx950 (no device needed).  0 on success.
+int compile_source(const std::string &src, std::vector<char> &code, std::string &log);
+
+// Names: encoder group (k, m, rt, depth, first parity row, rows per block)
+// and decoder group (n, pattern hash, rt, depth, group, rows per block).
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb);
+std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb);
+// Output-row groups [lo, hi), one hiprtc program each (large matrices are
 // split so each program stays near 4096 coefficients).
-std::vector<std::pair<int, int>> encode_groups(size_t k, size_t m, int rt);
-inline int fused_depth(int depth) { return depth < 2 ? depth : 2; }
-// HIP source of the module: the encode kernel and the frame+encode kernel;
-// parity_rows = the m x k parity block of the encoding matrix (rows k..k+m-1
-// of rse build_matrix), row-major; `depth` = data rows in flight ahead of
-// the one being multiplied.
-std::string gen_encode_source(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
-                              int r_lo, int r_hi);
-// hiprtc-compile one group for gfx950 (no device needed).  0 on success.
-int compile_encode(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth, int r_lo,
-                   int r_hi, std::vector<char> &code, std::string &log);
+std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt);
 
 }  // namespace hbrbc

@@ -73,19 +73,18 @@ __device__ __forceinline__ uint4 load16_shifted(const uint8_t *src, uint32_t sh)
 
 // One thread per 16-byte chunk of every data row; the (instance, row) of a
 // workgroup is scalar.  Logical framed byte b (= BE32(len) ++ payload ++ 0s)
-// lives in row b / S at b % S (broadcast.rs:174-189); [S, stride) is zeroed.
+// lives in row b / S at b % S (broadcast.rs:174-189); [S, round16(S)) is zeroed.
 __global__ __launch_bounds__(kBlock) void frame_kernel(
     const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P,
-    uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
+    uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
     uint32_t k, uint32_t blocks_per_row) {
     const uint32_t grow = blockIdx.x / blocks_per_row;  // instance * k + j
     const uint32_t chunk = (blockIdx.x - grow * blocks_per_row) * kBlock + threadIdx.x;
     const uint32_t off = chunk * 16;
-    if (off >= shard_stride) return;
+    if (off >= ((S + 15u) & ~15u)) return;
     const size_t inst = grow / k;
     const uint32_t j = grow - (uint32_t)inst * k;
-    uint4 *dst = reinterpret_cast<uint4 *>(shards + inst * inst_stride + (size_t)j * shard_stride +
-                                           off);
+    uint4 *dst = reinterpret_cast<uint4 *>(shards + inst * inst_stride + rows.off(j) + off);
     if (off >= S) {
         *dst = make_uint4(0, 0, 0, 0);
         return;
@@ -142,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void frame_kernel(
 // fused launch computed).  One thread per instance.
 __global__ __launch_bounds__(kBlock) void frame_fixup_kernel(
     const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P,
-    uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
+    uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
     uint32_t k, uint32_t m, const uint8_t *__restrict__ matrix, size_t count) {
     const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
     if (inst >= count) return;
@@ -151,84 +150,11 @@ __global__ __launch_bounds__(kBlock) void frame_fixup_kernel(
     for (uint32_t t = P & ~3u; t < P; ++t) {
         const uint8_t v = pay[t];
         const uint32_t b = t + 4, j = b / S, pos = b - j * S;
-        ib[(size_t)j * shard_stride + pos] = v;
+        ib[rows.off(j) + pos] = v;
         if (!v) continue;
         for (uint32_t r = 0; r < m; ++r) {
             const uint8_t c = matrix[(size_t)(k + r) * k + j];
-            if (c) ib[(size_t)(k + r) * shard_stride + pos] ^= kGf.exp[kGf.log[c] + kGf.log[v]];
-        }
-    }
-}
-
-// -------------------------------------------------------------- GF apply --
-// Split-2-bit v_perm_b32 GF(2^8) multiply-accumulate over 16-byte chunks.
-// Every lane owns 16 consecutive byte positions of all rows.  Output rows
-// are produced RT at a time ("passes"); the tables are pass-major
-// [pass][input j][RT] so the RT entries for one input arrive as wide scalar
-// loads.  Per (row, input, dword): 4 v_perm_b32 + 2 v_bitop3 (xor3) = 6 VALU
-// for 4 byte-MACs.  Rows past `nout` in the last pass carry zero entries;
-// only their stores are skipped.
-template <int RT>
-__global__ __launch_bounds__(kBlock) void gf_apply_kernel(
-    uint8_t *__restrict__ base, size_t inst_stride, size_t shard_stride, int n16,
-    const uint4 *__restrict__ tables, size_t tab_inst_stride,
-    const uint32_t *__restrict__ in_idx, size_t in_idx_stride,
-    const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
-    const int *__restrict__ nout_arr, int nout_uniform, int nin, int blocks_per_row) {
-    const size_t inst = blockIdx.x / blocks_per_row;
-    const int chunk0 = (int)(blockIdx.x % blocks_per_row) * kBlock + (int)threadIdx.x;
-    const bool active = chunk0 < n16;
-    const int chunk = active ? chunk0 : n16 - 1;  // clamped: loads stay in bounds
-    uint8_t *ib = base + inst * inst_stride;
-    const int nout = nout_arr ? nout_arr[inst] : nout_uniform;
-    const int npass = (nout + RT - 1) / RT;
-    const uint4 *tab = tables + inst * tab_inst_stride;
-    // 32-bit row indices: wave-uniform, so they come through the scalar cache
-    // (gfx950 has no sub-dword s_load; byte indices became vector loads whose
-    // vmcnt(0) drained the prefetch pipeline)
-    const uint32_t *iidx = in_idx + inst * in_idx_stride;
-    const uint32_t *oidx = out_idx + inst * out_idx_stride;
-    const size_t off = (size_t)chunk * 16;
-    for (int p = 0; p < npass; ++p) {
-        uint32_t acc[RT][4];
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) acc[t][d] = 0u;
-        const uint4 *tp = tab + (size_t)p * nin * RT;
-        uint4 xn = *reinterpret_cast<const uint4 *>(ib + (size_t)iidx[0] * shard_stride + off);
-        for (int j = 0; j < nin; ++j) {
-            const uint4 x = xn;
-            if (j + 1 < nin)
-                xn = *reinterpret_cast<const uint4 *>(ib + (size_t)iidx[j + 1] * shard_stride + off);
-            const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-            uint32_t sel[4][4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d)
-#pragma unroll
-                for (int f = 0; f < 4; ++f) sel[f][d] = (xs[d] >> (2 * f)) & 0x03030303u;
-            const uint4 *tj = tp + (size_t)j * RT;
-#pragma unroll
-            for (int t = 0; t < RT; ++t) {
-                const uint4 e = tj[t];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    acc[t][d] = xor3(acc[t][d], __builtin_amdgcn_perm(e.x, e.x, sel[0][d]),
-                                     __builtin_amdgcn_perm(e.y, e.y, sel[1][d]));
-                    acc[t][d] = xor3(acc[t][d], __builtin_amdgcn_perm(e.z, e.z, sel[2][d]),
-                                     __builtin_amdgcn_perm(e.w, e.w, sel[3][d]));
-                }
-            }
-        }
-        if (active) {
-#pragma unroll
-            for (int t = 0; t < RT; ++t) {
-                if (p * RT + t < nout) {
-                    const int dst = oidx[p * RT + t];
-                    *reinterpret_cast<uint4 *>(ib + (size_t)dst * shard_stride + off) =
-                        make_uint4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-                }
-            }
+            if (c) ib[rows.off(k + r) + pos] ^= kGf.exp[kGf.log[c] + kGf.log[v]];
         }
     }
 }
@@ -258,8 +184,7 @@ __device__ __forceinline__ void store16_stream(void *p, uint32_t a, uint32_t b, 
 // (2^b * x); doubling a bit-sliced value is three plane XORs (x^8 = 0x1D),
 // and each set coefficient bit costs 8 full-rate v_xor on 32 positions.
 // Coefficients are wave-uniform scalars, so "bit b of c set" is a scalar
-// branch: about 1 VALU op per byte-MAC against 6 VALU (4 half-rate v_perm)
-// per 4 byte-MACs in gf_apply_kernel.
+// branch: about 1 VALU op per byte-MAC.
 __device__ __forceinline__ void bs_transpose(uint32_t (&w)[8]) {
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
@@ -281,14 +206,20 @@ template <int RT, int MODE>
 // passes w, w + nwaves, ...  The waves read identical input bytes at the
 // same time, so only one copy comes from beyond L1/L2 (a lone wave running
 // its passes one after another re-read every input per pass: 3x the HBM/MALL
-// traffic at m = 42).
+// traffic at m = 42).  Instance i uses the coefficients and row lists of
+// slot pat[i] (the decode-matrix cache) or of slot i / the shared slot 0.
 __global__ __launch_bounds__(256) void gf_bitslice_kernel(
-    uint8_t *__restrict__ base, size_t inst_stride, size_t shard_stride, uint32_t row_bytes,
-    const uint8_t *__restrict__ coefs, size_t coef_inst_stride,
+    uint8_t *__restrict__ base, size_t inst_stride, RowMap rows, uint32_t row_bytes,
+    const uint8_t *__restrict__ coefs, size_t coef_slot_stride,
     const uint32_t *__restrict__ in_idx, size_t in_idx_stride,
     const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
-    const int *__restrict__ nout_arr, int nout_uniform, int nin, uint32_t waves_per_row) {
+    const int *__restrict__ nout_arr, int nout_uniform, const int *__restrict__ pat,
+    const uint64_t *__restrict__ slot_hash, uint64_t skip_hash, int hash_slots, int nin,
+    uint32_t waves_per_row) {
     const size_t inst = blockIdx.x / waves_per_row;
+    const int slot = pat ? pat[inst] : (int)inst;
+    // instances of a pattern with a specialised decoder are left to it
+    if (skip_hash && slot < hash_slots && slot_hash[slot] == skip_hash) return;
     const int wave = (int)(threadIdx.x >> 6), nwaves = (int)(blockDim.x >> 6);
     const uint32_t chunk = (blockIdx.x - (uint32_t)inst * waves_per_row) * 64 + (threadIdx.x & 63);
     uint32_t off = chunk * 32;
@@ -296,14 +227,14 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
     if (!active) off = row_bytes - 16;              // clamped, loads stay in the row
     const bool full = off + 32 <= row_bytes;        // else only 16 bytes belong to this row
     uint8_t *ib = base + inst * inst_stride;
-    const int nout = nout_arr ? nout_arr[inst] : nout_uniform;
+    const int nout = nout_arr ? nout_arr[slot] : nout_uniform;
     const int npass = (nout + RT - 1) / RT;
-    const uint8_t *cf = coefs + inst * coef_inst_stride;
+    const uint8_t *cf = coefs + (size_t)slot * coef_slot_stride;
     // 32-bit row indices: wave-uniform, so they come through the scalar cache
     // (gfx950 has no sub-dword s_load; byte indices became vector loads whose
     // vmcnt(0) drained the prefetch pipeline)
-    const uint32_t *iidx = in_idx + inst * in_idx_stride;
-    const uint32_t *oidx = out_idx + inst * out_idx_stride;
+    const uint32_t *iidx = in_idx + (size_t)slot * in_idx_stride;
+    const uint32_t *oidx = out_idx + (size_t)slot * out_idx_stride;
     for (int p = __builtin_amdgcn_readfirstlane(wave); p < npass; p += nwaves) {
         uint32_t acc[RT][8];
 #pragma unroll
@@ -318,7 +249,7 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
         // Loads are unconditional (index clamped, a half chunk re-reads its own
         // 16 bytes) so hipcc can count vmcnt exactly instead of draining.
         auto load_in = [&](int jj, uint4 &l, uint4 &h) {
-            const uint8_t *src = ib + (size_t)iidx[jj < nin ? jj : nin - 1] * shard_stride + off;
+            const uint8_t *src = ib + rows.off(iidx[jj < nin ? jj : nin - 1]) + off;
             l = *reinterpret_cast<const uint4 *>(src);
             h = *reinterpret_cast<const uint4 *>(src + (full ? 16 : 0));
         };
@@ -369,7 +300,7 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
             for (int t = 0; t < RT; ++t) {
                 if (p * RT + t < nout) {
                     bs_transpose(acc[t]);
-                    uint8_t *dst = ib + (size_t)oidx[p * RT + t] * shard_stride + off;
+                    uint8_t *dst = ib + rows.off(oidx[p * RT + t]) + off;
                     store16_stream(dst, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
                     if (full) store16_stream(dst + 16, acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
                 }
@@ -382,15 +313,45 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
 // One SHA3-256 sponge per lane: lane g hashes shard (g % n) of instance
 // (g / n).  All lanes share the shard length, so every branch is uniform.
 __global__ __launch_bounds__(kBlock) void leaf_hash_kernel(
-    const uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
     uint32_t n, size_t total, uint8_t *__restrict__ nodes, size_t node_inst_stride) {
     const size_t g = blockIdx.x * (size_t)kBlock + threadIdx.x;
     if (g >= total) return;
     const size_t inst = g / n;
     const uint32_t i = (uint32_t)(g - inst * n);
     uint32_t d[8];
-    sha3_256_row(shards + inst * inst_stride + (size_t)i * shard_stride, S, d);
+    sha3_256_row(shards + inst * inst_stride + rows.off(i), S, d);
     store_digest(nodes + inst * node_inst_stride + (size_t)i * 32, d);
+}
+
+// The rows a reconstruct rebuilt, compacted into one list: entry e = (instance,
+// row).  One thread per instance appends its slot's out_idx rows.
+__global__ __launch_bounds__(kBlock) void rebuilt_list_kernel(
+    size_t count, const int *__restrict__ pat, const uint32_t *__restrict__ out_idx,
+    size_t out_idx_stride, const int *__restrict__ nout, uint32_t *__restrict__ counter,
+    uint2 *__restrict__ list) {
+    const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
+    if (inst >= count) return;
+    const int slot = pat[inst];
+    const int no = nout[slot];
+    if (no <= 0) return;
+    const uint32_t at = atomicAdd(counter, (uint32_t)no);
+    const uint32_t *oi = out_idx + (size_t)slot * out_idx_stride;
+    for (int t = 0; t < no; ++t) list[at + t] = make_uint2((uint32_t)inst, oi[t]);
+}
+
+// SHA3 of the listed rows (a grid sized for the worst case; lanes past the
+// list length exit at once, so every wave that hashes is full).
+__global__ __launch_bounds__(kBlock) void leaf_hash_list_kernel(
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
+    const uint2 *__restrict__ list, const uint32_t *__restrict__ counter,
+    uint8_t *__restrict__ nodes, size_t node_inst_stride) {
+    const size_t g = blockIdx.x * (size_t)kBlock + threadIdx.x;
+    if (g >= *counter) return;
+    const uint2 e = list[g];
+    uint32_t d[8];
+    sha3_256_row(shards + e.x * inst_stride + rows.off(e.y), S, d);
+    store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
 }
 
 __global__ __launch_bounds__(kBlock) void ragged_hash_kernel(
@@ -452,22 +413,27 @@ __global__ __launch_bounds__(kBlock) void proofs_kernel(
 }
 
 // -------------------------------------------------------------- validate --
+// Proof::validate (merkle.rs:83-103) for proof (i, jj); see ValidateArgs.
 __global__ __launch_bounds__(kBlock) void validate_kernel(
-    const uint8_t *__restrict__ values, uint32_t value_len, size_t value_stride,
-    size_t value_inst_stride, uint32_t per_inst, const uint32_t *__restrict__ indices,
-    const uint8_t *__restrict__ digests, uint32_t dslots, const uint8_t *__restrict__ ndig,
-    const uint8_t *__restrict__ roots, size_t root_stride, uint32_t tree_n, size_t count,
-    uint8_t *__restrict__ ok_out) {
+    const uint8_t *__restrict__ values, uint32_t value_len, size_t value_inst_stride,
+    RowMap vrows, uint32_t per_inst, const uint32_t *__restrict__ rows,
+    const uint32_t *__restrict__ indices, const uint8_t *__restrict__ digests, uint32_t dslots,
+    uint32_t dig_rows, const uint8_t *__restrict__ ndig, const uint8_t *__restrict__ roots,
+    size_t root_stride, uint32_t tree_n, size_t count, uint8_t *__restrict__ ok_out,
+    uint8_t *__restrict__ leaf_out, size_t leaf_inst_stride) {
     const size_t g = blockIdx.x * (size_t)kBlock + threadIdx.x;
     if (g >= count * per_inst) return;
     const size_t inst = g / per_inst;
-    const uint32_t j = (uint32_t)(g - inst * per_inst);
+    const uint32_t jj = (uint32_t)(g - inst * per_inst);
+    const uint32_t r = rows ? rows[jj] : jj;
     uint32_t d[8];
-    sha3_256_row(values + inst * value_inst_stride + (size_t)j * value_stride, value_len, d);
-    uint32_t i = indices ? indices[g] : j;
+    sha3_256_row(values + inst * value_inst_stride + vrows.off(r), value_len, d);
+    if (leaf_out) store_digest(leaf_out + inst * leaf_inst_stride + (size_t)r * 32, d);
+    uint32_t i = indices ? indices[g] : r;
     uint32_t lvl_n = tree_n, used = 0;
-    const uint32_t nd = ndig[g];
-    const uint8_t *dig = digests + g * dslots * 32;
+    const size_t ps = inst * dig_rows + (rows ? r : jj);   // proof slot
+    const uint32_t nd = ndig[ps];
+    const uint8_t *dig = digests + ps * dslots * 32;
     bool ok = true;
     while (lvl_n > 1) {
         if ((i ^ 1u) < lvl_n) {
@@ -489,37 +455,118 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(
         lvl_n = (lvl_n + 1) >> 1;
     }
     if (used != nd) ok = false;  // too many levels in the proof
-    uint32_t r[8];
-    load_digest(roots + inst * root_stride, r);
+    uint32_t rt[8];
+    load_digest(roots + inst * root_stride, rt);
 #pragma unroll
-    for (int w = 0; w < 8; ++w) ok = ok && (r[w] == d[w]);
+    for (int w = 0; w < 8; ++w) ok = ok && (rt[w] == d[w]);
     ok_out[g] = ok ? 1 : 0;
 }
 
-// --------------------------------------------------------- decode matrix --
-// One workgroup per instance: first-k-present selection (rse reconstruct),
-// Gauss-Jordan inverse of M[valid] in LDS, recovery rows R = M[missing] *
-// inv(M[valid]) (missing data rows are rows of the inverse; missing parity
-// rows equal rse's parity-from-rebuilt-data by linearity over GF(2^8)),
-// expanded to split-2-bit tables for gf_apply_kernel.
+// --------------------------------------------------- decode-matrix cache --
+// Present mask of instance `inst` as 8 words (bit b of word w = present[32w+b]).
+__device__ __forceinline__ uint32_t mask_word(const uint8_t *pres, int n, int w) {
+    uint32_t v = 0;
+    for (int b = 0; b < 32; ++b) {
+        const int i = 32 * w + b;
+        if (i < n && pres[i]) v |= 1u << b;
+    }
+    return v;
+}
+
+__host__ __device__ __forceinline__ uint64_t pat_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t pat_hash_words(const uint32_t (&w)[8], int n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    for (int i = 0; i < 8; ++i) h = pat_mix(h + ((uint64_t)w[i] << 1) + (uint64_t)i);
+    return h ? h : 1ull;
+}
+
+// One thread per instance: the slot of its present pattern.  A hit (same
+// 64-bit hash) joins the slot; an empty slot is claimed by CAS (this
+// instance then computes it); a table at half load or 32 probes without
+// success send the instance to its private slot cap + inst.
+__global__ __launch_bounds__(kBlock) void pattern_lookup_kernel(
+    int n, const uint8_t *__restrict__ present, size_t count, PatternCache c,
+    int *__restrict__ pat, uint8_t *__restrict__ own) {
+    const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
+    if (inst >= count) return;
+    const uint8_t *pres = present + inst * (size_t)n;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = mask_word(pres, n, i);
+    const uint64_t h = pat_hash_words(w, n);
+    const bool may_insert = *reinterpret_cast<volatile uint32_t *>(c.fill) < (uint32_t)(c.cap / 2);
+    int slot = (int)(h & (uint64_t)(c.cap - 1)), found = -1, mine = 0;
+    for (int probe = 0; probe < 32; ++probe) {
+        unsigned long long cur = reinterpret_cast<volatile unsigned long long *>(c.hash)[slot];
+        if (cur == 0 && may_insert) {
+            cur = atomicCAS(reinterpret_cast<unsigned long long *>(c.hash) + slot, 0ull,
+                            (unsigned long long)h);
+            if (cur == 0) {
+                found = slot;
+                mine = 1;
+                atomicAdd(c.fill, 1u);
+                break;
+            }
+        }
+        if (cur == h) {
+            found = slot;
+            break;
+        }
+        if (cur == 0) break;  // empty and full table: not cached
+        slot = (slot + 1) & (c.cap - 1);
+    }
+    if (found < 0) {
+        found = c.cap + (int)inst;
+        mine = 1;
+    }
+    if (mine) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c.keys[(size_t)found * 8 + i] = w[i];
+    }
+    pat[inst] = found;
+    own[inst] = (uint8_t)mine;
+}
+
+// One workgroup per instance.  Instances that joined a slot verify its key
+// (a 64-bit hash collision moves them to their private slot) and stop; the
+// instance that owns a slot computes it: first-k-present selection (rse
+// reconstruct), Gauss-Jordan inverse of M[valid] in LDS, recovery rows
+// M[missing] * inv(M[valid]) (missing data rows are rows of the inverse;
+// missing parity rows equal rse's parity-from-rebuilt-data by linearity over
+// GF(2^8)), as coefficient bytes [pass][k][16] for gf_bitslice_kernel.
 __global__ __launch_bounds__(1024) void decode_matrix_kernel(
-    int n, int k, int rt, int raw, const uint8_t *__restrict__ matrix,
-    const uint8_t *__restrict__ present, uint4 *__restrict__ tables,
-    uint32_t *__restrict__ in_idx, uint32_t *__restrict__ out_idx, int *__restrict__ nout,
-    int32_t *__restrict__ status) {
+    int n, int k, int rt, const uint8_t *__restrict__ matrix, const uint8_t *__restrict__ present,
+    PatternCache c, int *__restrict__ pat, const uint8_t *__restrict__ own) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *exp_t = smem;             // 512
     uint8_t *log_t = smem + 512;       // 256
     uint8_t *valid = smem + 768;       // 256
     uint8_t *missing = smem + 1024;    // 256
     uint8_t *fac = smem + 1280;        // 256
-    int *meta = reinterpret_cast<int *>(smem + 1536);  // [0]=npresent [1]=nmiss [2]=pivot [3]=inv [4]=singular
+    int *meta = reinterpret_cast<int *>(smem + 1536);  // [0]=npresent [1]=nmiss [2]=pivot [3]=inv [4]=singular [5]=slot
     uint8_t *aug = smem + 1600;        // k x 2k
     const int m = n - k;
     const size_t inst = blockIdx.x;
     const int tid = threadIdx.x;
     const int nt = (int)blockDim.x;  // 64, 256 or 512 threads by k (launch_decode_matrix)
     const uint8_t *pres = present + inst * (size_t)n;
+    int slot = pat[inst];
+    if (!own[inst]) {
+        if (tid < 64) {
+            const bool diff = tid < 8 && mask_word(pres, n, tid) != c.keys[(size_t)slot * 8 + tid];
+            const unsigned long long bal = __ballot(diff);
+            if (tid == 0) meta[5] = bal ? 1 : 0;
+        }
+        __syncthreads();
+        if (!meta[5]) return;          // the slot's owner computes it
+        slot = c.cap + (int)inst;      // hash collision: private slot
+        if (tid < 8) c.keys[(size_t)slot * 8 + tid] = mask_word(pres, n, tid);
+        if (tid == 0) pat[inst] = slot;
+    }
 
     for (int i = tid; i < 512; i += nt) exp_t[i] = kGf.exp[i];
     for (int i = tid; i < 256; i += nt) log_t[i] = kGf.log[i];
@@ -541,23 +588,23 @@ __global__ __launch_bounds__(1024) void decode_matrix_kernel(
     const int np = meta[0], nm = meta[1];
     if (np == n || np < k) {
         if (tid == 0) {
-            nout[inst] = 0;
-            status[inst] = (np < k) ? 10 /* TooFewShardsPresent */ : 0;
+            c.nout[slot] = 0;
+            c.status[slot] = (np < k) ? 10 /* TooFewShardsPresent */ : 0;
         }
         return;
     }
     const int w2 = 2 * k;
     for (int e = tid; e < k * w2; e += nt) {
-        const int r = e / w2, c = e - r * w2;
-        aug[e] = (c < k) ? matrix[(size_t)valid[r] * k + c] : (uint8_t)((c - k) == r);
+        const int r = e / w2, col = e - r * w2;
+        aug[e] = (col < k) ? matrix[(size_t)valid[r] * k + col] : (uint8_t)((col - k) == r);
     }
     __syncthreads();
-    for (int c = 0; c < k; ++c) {
-        if (tid < 64) {   // pivot: first nonzero row at or below c, by ballot over 64 rows
+    for (int col0 = 0; col0 < k; ++col0) {
+        if (tid < 64) {   // pivot: first nonzero row at or below col0, by ballot over 64 rows
             int p = -1;
-            for (int r0 = c; r0 < k && p < 0; r0 += 64) {
+            for (int r0 = col0; r0 < k && p < 0; r0 += 64) {
                 const int r = r0 + tid;
-                const unsigned long long bal = __ballot(r < k && aug[r * w2 + c] != 0);
+                const unsigned long long bal = __ballot(r < k && aug[r * w2 + col0] != 0);
                 if (bal) p = r0 + __ffsll((long long)bal) - 1;
             }
             if (tid == 0) meta[2] = p;
@@ -567,77 +614,80 @@ __global__ __launch_bounds__(1024) void decode_matrix_kernel(
             if (p < 0)
                 meta[4] = 1;
             else
-                meta[3] = gf_inv_lds(exp_t, log_t, aug[p * w2 + c]);
+                meta[3] = gf_inv_lds(exp_t, log_t, aug[p * w2 + col0]);
         }
         __syncthreads();
         if (meta[4]) {
             if (tid == 0) {
-                nout[inst] = 0;
-                status[inst] = 64;  // SingularMatrix (impossible for an MDS code)
+                c.nout[slot] = 0;
+                c.status[slot] = 64;  // SingularMatrix (impossible for an MDS code)
             }
             return;
         }
         const int p = meta[2];
         const uint8_t inv = (uint8_t)meta[3];
-        if (p != c) {
+        if (p != col0) {
             for (int col = tid; col < w2; col += nt) {
-                uint8_t t = aug[c * w2 + col];
-                aug[c * w2 + col] = aug[p * w2 + col];
+                uint8_t t = aug[col0 * w2 + col];
+                aug[col0 * w2 + col] = aug[p * w2 + col];
                 aug[p * w2 + col] = t;
             }
         }
         __syncthreads();
         for (int col = tid; col < w2; col += nt)
-            aug[c * w2 + col] = gf_mul_lds(exp_t, log_t, inv, aug[c * w2 + col]);
+            aug[col0 * w2 + col] = gf_mul_lds(exp_t, log_t, inv, aug[col0 * w2 + col]);
         __syncthreads();
-        for (int r = tid; r < k; r += nt) fac[r] = (r == c) ? 0 : aug[r * w2 + c];
+        for (int r = tid; r < k; r += nt) fac[r] = (r == col0) ? 0 : aug[r * w2 + col0];
         __syncthreads();
         for (int e = tid; e < k * w2; e += nt) {
             const int r = e / w2, col = e - r * w2;
             const uint8_t f = fac[r];
-            if (f) aug[e] ^= gf_mul_lds(exp_t, log_t, f, aug[c * w2 + col]);
+            if (f) aug[e] ^= gf_mul_lds(exp_t, log_t, f, aug[col0 * w2 + col]);
         }
         __syncthreads();
     }
-    const int npass = (m + rt - 1) / rt;
-    uint4 *tab = tables + inst * (size_t)npass * rt * k;
+    uint8_t *tab = c.coefs + (size_t)slot * c.coef_stride;
     const int nrows = (nm + rt - 1) / rt * rt;  // pad the last pass with zero rows
     for (int e = tid; e < nrows * k; e += nt) {
-        const int t = e / k, c = e - t * k;
+        const int t = e / k, col = e - t * k;
         const int row = t < nm ? missing[t] : -1;
         uint8_t coef;
         if (row < 0) {
             coef = 0;
         } else if (row < k) {
-            coef = aug[row * w2 + k + c];
+            coef = aug[row * w2 + k + col];
         } else {
             coef = 0;
             const uint8_t *mr = matrix + (size_t)row * k;
-            for (int j = 0; j < k; ++j) coef ^= gf_mul_lds(exp_t, log_t, mr[j], aug[j * w2 + k + c]);
+            for (int j = 0; j < k; ++j) coef ^= gf_mul_lds(exp_t, log_t, mr[j], aug[j * w2 + k + col]);
         }
-        if (raw)  // bit-sliced kernel: coefficient bytes [pass][j][16]
-            reinterpret_cast<uint8_t *>(tab)[((size_t)(t / rt) * k + c) * 16 + (t % rt)] = coef;
-        else      // perm kernel: split-2-bit entries [pass][j][rt]
-            tab[((size_t)(t / rt) * k + c) * rt + (t % rt)] = gf_split2_entry(coef, exp_t, log_t);
+        tab[((size_t)(t / rt) * k + col) * 16 + (t % rt)] = coef;  // [pass][j][16]
     }
-    for (int j = tid; j < k; j += nt) in_idx[inst * (size_t)k + j] = valid[j];
-    for (int t = tid; t < nm; t += nt) out_idx[inst * (size_t)m + t] = missing[t];
+    for (int j = tid; j < k; j += nt) c.in_idx[(size_t)slot * k + j] = valid[j];
+    for (int t = tid; t < nm; t += nt) c.out_idx[(size_t)slot * m + t] = missing[t];
     if (tid == 0) {
-        nout[inst] = nm;
-        status[inst] = 0;
+        c.nout[slot] = nm;
+        c.status[slot] = 0;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void pattern_status_kernel(
+    size_t count, const int *__restrict__ pat, const int32_t *__restrict__ slot_status,
+    int32_t *__restrict__ status) {
+    const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
+    if (inst < count) status[inst] = slot_status[pat[inst]];
 }
 
 // ---------------------------------------------------------- decode check --
 __device__ __forceinline__ uint8_t logical_byte(const uint8_t *ib, uint64_t b, uint32_t S,
-                                                size_t shard_stride) {
-    return ib[(b / S) * shard_stride + (b % S)];
+                                                const RowMap &rows) {
+    return ib[rows.off((uint32_t)(b / S)) + (b % S)];
 }
 
 __global__ __launch_bounds__(kBlock) void decode_check_kernel(
     const int32_t *__restrict__ recon_status, const uint8_t *__restrict__ nodes,
     size_t node_inst_stride, uint32_t root_node, const uint8_t *__restrict__ roots,
-    size_t root_stride, const uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride,
+    size_t root_stride, const uint8_t *__restrict__ shards, uint32_t S, RowMap rows,
     size_t inst_stride, uint32_t k, size_t count, uint32_t *__restrict__ plen_out,
     int32_t *__restrict__ status_out) {
     const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
@@ -659,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void decode_check_kernel(
         } else {
             const uint8_t *ib = shards + inst * inst_stride;
             uint32_t v = 0;
-            for (int q = 0; q < 4; ++q) v = (v << 8) | logical_byte(ib, (uint64_t)q, S, shard_stride);
+            for (int q = 0; q < 4; ++q) v = (v << 8) | logical_byte(ib, (uint64_t)q, S, rows);
             len = (uint32_t)min<uint64_t>((uint64_t)v, total - 4);  // take() truncates
         }
     }
@@ -668,59 +718,60 @@ __global__ __launch_bounds__(kBlock) void decode_check_kernel(
 }
 
 // --------------------------------------------------------------- unframe --
-// One thread per output dword: logical bytes 4 + 4w .. +3 of the
-// concatenated data rows.
 // One thread per 16 output bytes (payload bytes 16c..16c+15 = logical bytes
 // 4+16c.. of the concatenated data rows, broadcast.rs:590-598); the instance
-// of a workgroup is scalar.  Bytes past the decoded length are written 0.
+// of a workgroup is scalar.  Every chunk of the row is written: bytes past
+// the decoded length (all of them for a failed instance) are 0.
 __global__ __launch_bounds__(kBlock) void unframe_kernel(
-    const uint8_t *__restrict__ shards, uint32_t S, size_t shard_stride, size_t inst_stride,
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
     uint32_t k, const uint32_t *__restrict__ plen, const int32_t *__restrict__ status,
-    uint8_t *__restrict__ payload_out, size_t payload_stride, uint32_t blocks_per_inst) {
+    uint8_t *__restrict__ payload_out, size_t payload_stride, uint32_t chunks,
+    uint32_t blocks_per_inst) {
     const size_t inst = blockIdx.x / blocks_per_inst;
     const uint32_t c = (blockIdx.x - (uint32_t)inst * blocks_per_inst) * kBlock + threadIdx.x;
-    const uint32_t len = plen[inst];
+    if (c >= chunks) return;
+    const uint32_t len = status[inst] == 0 ? plen[inst] : 0u;
     const uint32_t o = c * 16;
-    if (status[inst] != 0 || o >= len) return;
-    const uint64_t total = (uint64_t)k * S;
-    const uint8_t *ib = shards + inst * inst_stride;
-    const uint64_t lb = 4 + (uint64_t)o;
-    const uint32_t row = (uint32_t)(lb / S);
-    const uint32_t off = (uint32_t)(lb - (uint64_t)row * S);
-    uint32_t w[4];
-    // Chunks inside one row share a misalignment: when the wave agrees, two
-    // aligned 16-byte loads (coalesced) and a register shift.  off + 16 <= S
-    // <= stride keeps the second 16 bytes inside the row when sh != 0.
-    const uint32_t sh = off & 15u;
-    const uint32_t sh0 = __builtin_amdgcn_readfirstlane(sh);
-    if (__all(off + 16 <= S && sh == sh0)) {
-        const uint4 v = load16_shifted(ib + (size_t)row * shard_stride + (off - sh), sh0);
-        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-    } else if (off + 16 <= S) {
-        // inside one row; the fifth dword ends at most 3 bytes past S (< stride)
-        const uint32_t *rw =
-            reinterpret_cast<const uint32_t *>(ib + (size_t)row * shard_stride) + (off >> 2);
-        const uint32_t sh = (off & 3) * 8;
-        uint32_t d[5];
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (o < len) {
+        const uint64_t total = (uint64_t)k * S;
+        const uint8_t *ib = shards + inst * inst_stride;
+        const uint64_t lb = 4 + (uint64_t)o;
+        const uint32_t row = (uint32_t)(lb / S);
+        const uint32_t off = (uint32_t)(lb - (uint64_t)row * S);
+        // Chunks inside one row share a misalignment: when the wave agrees, two
+        // aligned 16-byte loads (coalesced) and a register shift.  off + 16 <= S
+        // <= row slot keeps the second 16 bytes inside the row when sh != 0.
+        const uint32_t sh = off & 15u;
+        const uint32_t sh0 = __builtin_amdgcn_readfirstlane(sh);
+        const uint8_t *rp = ib + rows.off(row);
+        if (__all(off + 16 <= S && sh == sh0)) {
+            const uint4 v = load16_shifted(rp + (off - sh), sh0);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else if (off + 16 <= S) {
+            // inside one row; the fifth dword ends at most 3 bytes past S (< slot)
+            const uint32_t *rw = reinterpret_cast<const uint32_t *>(rp) + (off >> 2);
+            const uint32_t s8 = (off & 3) * 8;
+            uint32_t d[5];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = rw[q];
-        d[4] = sh ? rw[4] : 0u;
-        const uint4 v = funnel16(d, sh);
-        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-    } else {
-        w[0] = w[1] = w[2] = w[3] = 0;
-        for (int q = 0; q < 16; ++q) {
-            const uint64_t b = lb + q;
-            if (b < total) w[q >> 2] |= (uint32_t)logical_byte(ib, b, S, shard_stride) << (8 * (q & 3));
+            for (int q = 0; q < 4; ++q) d[q] = rw[q];
+            d[4] = s8 ? rw[4] : 0u;
+            const uint4 v = funnel16(d, s8);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+            for (int q = 0; q < 16; ++q) {
+                const uint64_t b = lb + q;
+                if (b < total) w[q >> 2] |= (uint32_t)logical_byte(ib, b, S, rows) << (8 * (q & 3));
+            }
         }
-    }
-    const uint32_t nb = len - o;  // bytes of this chunk inside the payload
-    if (nb < 16) {
+        const uint32_t nb = len - o;  // bytes of this chunk inside the payload
+        if (nb < 16) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int keep = (int)nb - 4 * q;
-            if (keep <= 0) w[q] = 0;
-            else if (keep < 4) w[q] &= 0xFFFFFFFFu >> (8 * (4 - keep));
+            for (int q = 0; q < 4; ++q) {
+                const int keep = (int)nb - 4 * q;
+                if (keep <= 0) w[q] = 0;
+                else if (keep < 4) w[q] &= 0xFFFFFFFFu >> (8 * (4 - keep));
+            }
         }
     }
     uint32_t *dst = reinterpret_cast<uint32_t *>(payload_out + inst * payload_stride + o);
@@ -764,6 +815,13 @@ size_t shaped_lds(size_t lanes, int max_w) {
 constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kernels (<= 128 VGPRs)
 }  // namespace
 
+uint64_t pattern_hash(const uint8_t *present, int n) {
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n && i < 256; ++i)
+        if (present[i]) w[i / 32] |= 1u << (i % 32);
+    return pat_hash_words(w, n);
+}
+
 hipError_t configure_kernels() {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -772,6 +830,7 @@ hipError_t configure_kernels() {
     if (e != hipSuccess) return e;
     for (const void *k : {reinterpret_cast<const void *>(decode_matrix_kernel),
                           reinterpret_cast<const void *>(leaf_hash_kernel),
+                          reinterpret_cast<const void *>(leaf_hash_list_kernel),
                           reinterpret_cast<const void *>(validate_kernel)}) {
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
@@ -780,98 +839,68 @@ hipError_t configure_kernels() {
 }
 
 hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
-                        size_t count, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                        size_t count, uint8_t *shards, size_t shard_len, const RowMap &rows,
                         size_t inst_stride, size_t data_shards, hipStream_t s) {
-    const size_t chunks = shard_stride / 16;
+    const size_t chunks = (shard_len + 15) / 16;
     if (count == 0 || chunks == 0) return hipSuccess;
     const size_t bpr = (chunks + kBlock - 1) / kBlock;
     const size_t blocks = bpr * count * data_shards;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(frame_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, payloads,
-                       payload_stride, (uint32_t)payload_len, shards, (uint32_t)shard_len,
-                       shard_stride, inst_stride, (uint32_t)data_shards, (uint32_t)bpr);
+                       payload_stride, (uint32_t)payload_len, shards, (uint32_t)shard_len, rows,
+                       inst_stride, (uint32_t)data_shards, (uint32_t)bpr);
     return hipGetLastError();
 }
 
 hipError_t launch_frame_fixup(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
-                              uint8_t *shards, size_t shard_len, size_t shard_stride,
+                              uint8_t *shards, size_t shard_len, const RowMap &rows,
                               size_t inst_stride, size_t k, size_t m, const uint8_t *matrix,
                               size_t count, hipStream_t s) {
     if (count == 0 || (payload_len & 3) == 0) return hipSuccess;
     hipLaunchKernelGGL(frame_fixup_kernel, dim3(grid_for(count, (size_t)1 << 30)), dim3(kBlock), 0,
                        s, payloads, payload_stride, (uint32_t)payload_len, shards,
-                       (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)k, (uint32_t)m,
-                       matrix, count);
+                       (uint32_t)shard_len, rows, inst_stride, (uint32_t)k, (uint32_t)m, matrix,
+                       count);
     return hipGetLastError();
 }
 
 hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     if (a.count == 0 || a.n16 == 0) return hipSuccess;
     if (!a.nout && a.nout_uniform == 0) return hipSuccess;
-    if (a.bitslice) {
-        const uint32_t row_bytes = (uint32_t)a.n16 * 16;
-        const uint32_t wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
-        const size_t blocks = (size_t)wpr * a.count;
-        if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-        const uint8_t *coefs = reinterpret_cast<const uint8_t *>(a.tables);
-        const size_t cstride = a.tab_inst_stride * sizeof(uint4);
-        const int max_rows = a.nout ? a.max_rows : a.nout_uniform;
-        const int nw = std::max(1, std::min(4, (max_rows + a.rt - 1) / a.rt));  // waves per block
+    const uint32_t row_bytes = (uint32_t)a.n16 * 16;
+    const uint32_t wpr = (row_bytes + 64 * 32 - 1) / (64 * 32);
+    const size_t blocks = (size_t)wpr * a.count;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const int max_rows = a.nout ? a.max_rows : a.nout_uniform;
+    const int nw = std::max(1, std::min(4, (max_rows + a.rt - 1) / a.rt));  // waves per block
+#define HB_BS_LAUNCH(RT, MODE)                                                                   \
+    hipLaunchKernelGGL((gf_bitslice_kernel<RT, MODE>), dim3((unsigned)blocks), dim3(64 * nw), 0, \
+                       s, a.base, a.inst_stride, a.rows, row_bytes, a.coefs, a.coef_slot_stride, \
+                       a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,          \
+                       a.nout_uniform, a.pat, a.slot_hash, a.skip_hash, a.hash_slots, a.nin, wpr)
 #define HB_BS_CASE(RT)                                                                           \
     case RT:                                                                                     \
-        if (a.bitslice == 3)                                                                     \
-            hipLaunchKernelGGL((gf_bitslice_kernel<RT, 2>), dim3((unsigned)blocks), dim3(64 * nw), 0, s, \
-                               a.base, a.inst_stride, a.shard_stride, row_bytes, coefs, cstride, \
-                               a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,   \
-                               a.nout_uniform, a.nin, wpr);                                      \
-        else if (a.bitslice == 2)                                                                \
-            hipLaunchKernelGGL((gf_bitslice_kernel<RT, 1>), dim3((unsigned)blocks), dim3(64 * nw), 0, s, \
-                               a.base, a.inst_stride, a.shard_stride, row_bytes, coefs, cstride, \
-                               a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,   \
-                               a.nout_uniform, a.nin, wpr);                                      \
+        if (a.mode == 2)                                                                         \
+            HB_BS_LAUNCH(RT, 2);                                                                 \
+        else if (a.mode == 1)                                                                    \
+            HB_BS_LAUNCH(RT, 1);                                                                 \
         else                                                                                     \
-            hipLaunchKernelGGL((gf_bitslice_kernel<RT, 0>), dim3((unsigned)blocks), dim3(64 * nw), 0, s, \
-                               a.base, a.inst_stride, a.shard_stride, row_bytes, coefs, cstride, \
-                               a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,   \
-                               a.nout_uniform, a.nin, wpr);                                      \
-        break
-        switch (a.rt) {
-            HB_BS_CASE(2);
-            HB_BS_CASE(4);
-            HB_BS_CASE(6);
-            HB_BS_CASE(8);
-            HB_BS_CASE(10);
-            HB_BS_CASE(12);
-            HB_BS_CASE(14);
-            HB_BS_CASE(16);
-            default:
-                return hipErrorInvalidValue;
-        }
-#undef HB_BS_CASE
-        return hipGetLastError();
-    }
-    const int bpr = (a.n16 + kBlock - 1) / kBlock;
-    const size_t blocks = (size_t)bpr * a.count;
-#define HB_GF_CASE(RT)                                                                           \
-    case RT:                                                                                     \
-        hipLaunchKernelGGL(gf_apply_kernel<RT>, dim3((unsigned)blocks), dim3(kBlock), 0, s,      \
-                           a.base, a.inst_stride, a.shard_stride, a.n16, a.tables,               \
-                           a.tab_inst_stride, a.in_idx, a.in_idx_stride, a.out_idx,              \
-                           a.out_idx_stride, a.nout, a.nout_uniform, a.nin, bpr);                \
+            HB_BS_LAUNCH(RT, 0);                                                                 \
         break
     switch (a.rt) {
-        HB_GF_CASE(2);
-        HB_GF_CASE(4);
-        HB_GF_CASE(6);
-        HB_GF_CASE(8);
-        HB_GF_CASE(10);
-        HB_GF_CASE(12);
-        HB_GF_CASE(14);
-        HB_GF_CASE(16);
+        HB_BS_CASE(2);
+        HB_BS_CASE(4);
+        HB_BS_CASE(6);
+        HB_BS_CASE(8);
+        HB_BS_CASE(10);
+        HB_BS_CASE(12);
+        HB_BS_CASE(14);
+        HB_BS_CASE(16);
         default:
             return hipErrorInvalidValue;
     }
-#undef HB_GF_CASE
+#undef HB_BS_CASE
+#undef HB_BS_LAUNCH
     return hipGetLastError();
 }
 
@@ -883,14 +912,32 @@ int gf_row_tile(int rows) {
     return rt < 2 ? 2 : (rt > 16 ? 16 : rt);
 }
 
-hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, size_t shard_stride,
+hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                             size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
                             size_t node_inst_stride, hipStream_t s) {
     const size_t total = n * count;
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
-                       shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)n,
-                       total, nodes, node_inst_stride);
+                       shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len, rows,
+                       inst_stride, (uint32_t)n, total, nodes, node_inst_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_leaf_hash_rebuilt(const uint8_t *shards, size_t shard_len, const RowMap &rows,
+                                    size_t inst_stride, size_t count, const int *pat,
+                                    const uint32_t *out_idx, size_t out_idx_stride,
+                                    const int *nout, int max_rows, uint8_t *nodes,
+                                    size_t node_inst_stride, uint32_t *counter, uint2 *list,
+                                    hipStream_t s) {
+    if (count == 0 || max_rows <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rebuilt_list_kernel, dim3(grid_for(count, (size_t)1 << 30)), dim3(kBlock),
+                       0, s, count, pat, out_idx, out_idx_stride, nout, counter, list);
+    const size_t total = count * (size_t)max_rows;
+    hipLaunchKernelGGL(leaf_hash_list_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
+                       0, s, shards, (uint32_t)shard_len, rows, inst_stride, list, counter, nodes,
+                       node_inst_stride);
     return hipGetLastError();
 }
 
@@ -927,14 +974,18 @@ hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
     const size_t total = a.count * a.per_inst;
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(validate_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
-                       shaped_lds(total, kSpongeMaxWaves), s, a.values, (uint32_t)a.value_len, a.value_stride, a.value_inst_stride,
-                       (uint32_t)a.per_inst, a.indices, a.digests, (uint32_t)a.dslots, a.ndig,
-                       a.roots, a.root_stride, (uint32_t)a.tree_n, a.count, a.ok_out);
+                       shaped_lds(total, kSpongeMaxWaves), s, a.values, (uint32_t)a.value_len,
+                       a.value_inst_stride, a.vrows, (uint32_t)a.per_inst, a.rows, a.indices,
+                       a.digests, (uint32_t)a.dslots, (uint32_t)a.dig_rows, a.ndig, a.roots,
+                       a.root_stride, (uint32_t)a.tree_n, a.count, a.ok_out, a.leaf_out,
+                       a.leaf_inst_stride);
     return hipGetLastError();
 }
 
 hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
+    hipLaunchKernelGGL(pattern_lookup_kernel, dim3(grid_for(a.count, (size_t)1 << 30)),
+                       dim3(kBlock), 0, s, a.n, a.present, a.count, a.cache, a.pat, a.own);
     const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
     // threads per instance by system size (measured per step): k = 22 one
     // wave, 0.46 -> 0.34 ms (no cross-wave barriers, more instances per CU);
@@ -948,25 +999,27 @@ hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     const int threads = (force >= 64 && force <= 1024 && force % 64 == 0) ? force
                                                                          : (a.k <= 32 ? 64 : a.k <= 64 ? 256 : 512);
     hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(threads), lds, s, a.n,
-                       a.k, a.rt, a.raw, a.matrix, a.present, a.tables, a.in_idx, a.out_idx, a.nout, a.status);
+                       a.k, a.rt, a.matrix, a.present, a.cache, a.pat, a.own);
+    hipLaunchKernelGGL(pattern_status_kernel, dim3(grid_for(a.count, (size_t)1 << 30)),
+                       dim3(kBlock), 0, s, a.count, a.pat, a.cache.status, a.status);
     return hipGetLastError();
 }
 
 hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes,
                                size_t node_inst_stride, size_t root_node, const uint8_t *roots,
                                size_t root_stride, const uint8_t *shards, size_t shard_len,
-                               size_t shard_stride, size_t inst_stride, size_t data_shards,
+                               const RowMap &rows, size_t inst_stride, size_t data_shards,
                                size_t count, uint32_t *plen_out, int32_t *status_out,
                                hipStream_t s) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(decode_check_kernel, dim3(grid_for(count, (size_t)1 << 30)), dim3(kBlock),
                        0, s, recon_status, nodes, node_inst_stride, (uint32_t)root_node, roots,
-                       root_stride, shards, (uint32_t)shard_len, shard_stride, inst_stride,
+                       root_stride, shards, (uint32_t)shard_len, rows, inst_stride,
                        (uint32_t)data_shards, count, plen_out, status_out);
     return hipGetLastError();
 }
 
-hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, size_t shard_stride,
+hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                           size_t inst_stride, size_t data_shards, size_t count,
                           const uint32_t *plen, const int32_t *status, uint8_t *payload_out,
                           size_t payload_stride, hipStream_t s) {
@@ -977,8 +1030,8 @@ hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, size_t shard_
     const size_t blocks = bpi * count;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(unframe_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, shards,
-                       (uint32_t)shard_len, shard_stride, inst_stride, (uint32_t)data_shards,
-                       plen, status, payload_out, payload_stride, (uint32_t)bpi);
+                       (uint32_t)shard_len, rows, inst_stride, (uint32_t)data_shards, plen, status,
+                       payload_out, payload_stride, (uint32_t)chunks, (uint32_t)bpi);
     return hipGetLastError();
 }
 

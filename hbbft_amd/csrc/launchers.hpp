@@ -8,36 +8,66 @@
 
 namespace hbrbc {
 
+// Row placement inside one instance of a shard slab: row j sits at byte
+//   (j / rb) * bst + (j % rb) * sst
+// past the instance base.  rb >= n is the plain shard-major layout (row j at
+// j * sst, the reference's contiguous N*S buffer, broadcast.rs:184); rb < n
+// groups the rows in blocks of rb, e.g. the destination-major Value/Echo
+// slabs of the validator-sharded simulation ([rank][instance][rb][sst]).
+struct RowMap {
+    uint64_t sst = 0, bst = 0;
+    uint32_t rb = 0xFFFFFFFFu;
+    __host__ __device__ __forceinline__ uint64_t off(uint32_t j) const {
+        if (j < rb) return (uint64_t)j * sst;
+        const uint32_t q = j / rb;
+        return (uint64_t)q * bst + (uint64_t)(j - q * rb) * sst;
+    }
+    __host__ __device__ __forceinline__ bool plain() const { return rb == 0xFFFFFFFFu; }
+};
+inline RowMap plain_rows(size_t sst) {
+    RowMap r;
+    r.sst = sst;
+    return r;
+}
+
 // Frame `count` payloads into the data rows of a shard slab (zero padding).
 hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
-                        size_t count, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                        size_t count, uint8_t *shards, size_t shard_len, const RowMap &rows,
                         size_t inst_stride, size_t data_shards, hipStream_t s);
 
 // The last payload_len & 3 payload bytes of a fused frame+encode: data byte
 // plus its GF(2^8) contribution to every parity row (matrix = n x k, device).
 hipError_t launch_frame_fixup(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
-                              uint8_t *shards, size_t shard_len, size_t shard_stride,
+                              uint8_t *shards, size_t shard_len, const RowMap &rows,
                               size_t inst_stride, size_t k, size_t m, const uint8_t *matrix,
                               size_t count, hipStream_t s);
 
-// out_row[r] = sum_j C[r][j] * in_row[in_idx[j]] on 16-byte chunks, for
-// nout (per instance or uniform) output rows out_idx[r].
+// out_row[r] = sum_j C[r][j] * in_row[in_idx[j]] (bit-sliced GF(2^8)), for
+// nout (per pattern or uniform) output rows out_idx[r].  With `pat` the
+// coefficients, row lists and counts of instance i are those of slot pat[i]
+// (the decode-matrix cache); instances whose slot hash equals `skip_hash`
+// are left to a pattern-specialised kernel.
 struct GfApplyArgs {
     uint8_t *base;
-    size_t inst_stride, shard_stride;
+    size_t inst_stride;
+    RowMap rows;
     int n16;                    // 16-byte chunks per row
-    const uint4 *tables;        // split-2-bit entries [inst][pass][nin][rt]
-    size_t tab_inst_stride;     // in entries (0: shared)
-    const uint32_t *in_idx;     // [inst][nin]
+    const uint8_t *coefs;       // coefficient bytes [slot][pass][nin][16]
+    size_t coef_slot_stride;    // bytes (0: shared)
+    const uint32_t *in_idx;     // [slot][nin]
     size_t in_idx_stride;       // 0: shared
-    const uint32_t *out_idx;    // [inst][max_out]
+    const uint32_t *out_idx;    // [slot][max_out]
     size_t out_idx_stride;      // 0: shared
-    const int *nout;            // [inst] or nullptr
+    const int *nout;            // [slot] or nullptr
     int nout_uniform;
+    const int *pat;             // [inst] -> slot, or nullptr (slot = inst)
+    const uint64_t *slot_hash;  // [slot] (with skip_hash)
+    uint64_t skip_hash;         // 0: none
+    int hash_slots;             // slots < hash_slots have a slot_hash entry
     int max_rows;               // upper bound of nout[] (per-instance row counts)
     int nin;
     int rt;                     // rows per pass: one of 2,4,...,16
-    int bitslice;               // 1: gf_bitslice_kernel, tables = coefficient bytes [pass][nin][16]
+    int mode;                   // 0 branch per coefficient bit, 1 branch hinted, 2 masked
     size_t count;
 };
 // Row tile for `rows` output rows: fewest passes of <= 16, evened out.
@@ -45,9 +75,18 @@ int gf_row_tile(int rows);
 hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s);
 
 // SHA3 of every shard row -> level 0 of each instance's node slab.
-hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, size_t shard_stride,
+hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                             size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
                             size_t node_inst_stride, hipStream_t s);
+// SHA3 of only the rows a reconstruct rebuilt (out_idx of each instance's
+// decode-matrix slot) -> their level-0 nodes; the other leaves are already
+// there (decode with known leaves).
+hipError_t launch_leaf_hash_rebuilt(const uint8_t *shards, size_t shard_len, const RowMap &rows,
+                                    size_t inst_stride, size_t count, const int *pat,
+                                    const uint32_t *out_idx, size_t out_idx_stride,
+                                    const int *nout, int max_rows, uint8_t *nodes,
+                                    size_t node_inst_stride, uint32_t *counter, uint2 *list,
+                                    hipStream_t s);
 // SHA3 of ragged values: value v at base + offsets[v], lens[v] bytes
 // (offsets 8-byte aligned) -> out + 32*v.
 hipError_t launch_ragged_hash(const uint8_t *base, const uint64_t *offsets,
@@ -58,42 +97,69 @@ hipError_t launch_tree_level(uint8_t *nodes, size_t node_inst_stride, size_t pre
                              hipStream_t s);
 hipError_t launch_proofs(const uint8_t *nodes, size_t node_inst_stride, size_t n, size_t count,
                          uint8_t *digests, size_t dslots, uint8_t *ndig, hipStream_t s);
+// Proof (i, jj): value row r = rows ? rows[jj] : jj of instance i at
+// values + i*value_inst_stride + vrows.off(r); claimed index indices[i*per_inst
+// + jj] (nullptr: r); digests/ndig of proof slot i*dig_rows + (rows ? r : jj);
+// leaf_out (optional): SHA3(value) to leaf_out + i*leaf_inst_stride + r*32.
 struct ValidateArgs {
     const uint8_t *values;
-    size_t value_len, value_stride, value_inst_stride, per_inst;
+    size_t value_len, value_inst_stride, per_inst;
+    RowMap vrows;
+    const uint32_t *rows;
     const uint32_t *indices;
     const uint8_t *digests;
-    size_t dslots;
+    size_t dslots, dig_rows;
     const uint8_t *ndig;
     const uint8_t *roots;
     size_t root_stride, tree_n, count;
     uint8_t *ok_out;
+    uint8_t *leaf_out;
+    size_t leaf_inst_stride;
 };
 hipError_t launch_validate(const ValidateArgs &a, hipStream_t s);
 
-// Per-instance decode matrix: inv(M[first k present]) applied to
-// M[missing rows] -> split-2-bit tables + row index lists.
+// Decode-matrix cache (rse keeps an LRU of decode matrices keyed by the
+// erasure pattern, behind broadcast.rs:684).  Slot s holds the coefficient
+// bytes [pass][k][16], in_idx [k], out_idx [m], nout and status of one
+// present-pattern; slots [0, cap) are shared (open addressing on a 64-bit
+// hash of the present mask), slot cap + i is instance i's private slot
+// (table full or hash collision).
+struct PatternCache {
+    uint64_t *hash;             // [cap]: 0 empty
+    uint32_t *keys;             // [cap + count][8]: present bitmask
+    uint8_t *coefs;             // [cap + count][coef_stride]
+    size_t coef_stride;
+    uint32_t *in_idx;           // [cap + count][k]
+    uint32_t *out_idx;          // [cap + count][m]
+    int *nout;                  // [cap + count]
+    int32_t *status;            // [cap + count]
+    uint32_t *fill;             // shared slots claimed so far (device counter)
+    int cap;                    // power of two
+};
 struct DecodeMatrixArgs {
-    int n, k, rt, raw;          // raw: coefficient bytes for the bit-sliced kernel
+    int n, k, rt;
     const uint8_t *matrix;      // n x k encoding matrix (device)
     const uint8_t *present;     // [count][n]
     size_t count;
-    uint4 *tables;              // [count][ceil(m/rt)][k][rt]
-    uint32_t *in_idx;           // [count][k]
-    uint32_t *out_idx;          // [count][m]
-    int *nout;                  // [count]
-    int32_t *status;            // [count]
+    PatternCache cache;
+    int *pat;                   // [count] -> slot
+    uint8_t *own;               // [count]: this instance computes its slot
+    int32_t *status;            // [count] out
 };
+// lookup (slot per instance) -> decode matrix of new slots -> per-instance status
 hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s);
+// 64-bit hash of a present mask (as the lookup kernel computes it): lets the
+// host name the slot of a pattern it specialised a decoder for.
+uint64_t pattern_hash(const uint8_t *present, int n);
 
 // Root compare + BE32 length parse (decode_from_shards tail).
 hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes,
                                size_t node_inst_stride, size_t root_node, const uint8_t *roots,
                                size_t root_stride, const uint8_t *shards, size_t shard_len,
-                               size_t shard_stride, size_t inst_stride, size_t data_shards,
+                               const RowMap &rows, size_t inst_stride, size_t data_shards,
                                size_t count, uint32_t *plen_out, int32_t *status_out,
                                hipStream_t s);
-hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, size_t shard_stride,
+hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                           size_t inst_stride, size_t data_shards, size_t count,
                           const uint32_t *plen, const int32_t *status, uint8_t *payload_out,
                           size_t payload_stride, hipStream_t s);

@@ -8,37 +8,39 @@ step; local instance i of rank g has proposer g*R + (i mod |block g|).
 One step follows the messages of /root/reference/src/broadcast/broadcast.rs:
 
 1. proposer rank: frame + encode + Merkle tree + N proofs (send_shards,
-   170-225), all through libhbrbc.so.
+   170-225).  The encoder writes the shard slab destination-major,
+   [G][count][R][stride] (a blocked row layout of libhbrbc, hbrbc.h
+   "*_rows"), so block d is already the contiguous chunk that goes to rank d.
 2. Value (212-222): shard j with its proof goes to validator j, i.e. to rank
-   owner(j).  Over all instances that is an all-to-all of [G][count][R] shard
-   rows plus their digests (RCCL over xGMI when the group is NCCL).  The root
-   travels inside every proof; the roots are all-gathered (the Ready/EchoHash
-   fan-out of 32-byte digests).
+   owner(j): one all-to-all of the slab (RCCL over xGMI when the group is
+   NCCL), one of the digests; the roots are all-gathered (the 32-byte
+   Ready/EchoHash fan-out).
 3. every validator validates its Value (handle_value -> validate_proof,
-   254 / 604-606): one Proof::validate per (instance, validator).
-4. Echo (send_echo_left, 413-425): validator j sends its shard and proof to the
-   N-f nodes on its left.  The simulated receiver of each instance is the
-   proposer's own node p, which gets Echoes from every validator except its
-   f right-hand neighbours p+1..p+f (right_nodes, 476-485) and except
-   validators whose Value failed validation (they send no Echo, 254-256).
-   The Echo rows go back to the proposer's rank: a second all-to-all.
-5. the receiver decodes (compute_output -> decode_from_shards, 526-601):
-   reconstruct, re-tree, root compare, unframe.
+   254 / 604-606): one Proof::validate per (instance, validator), which also
+   yields the row's Merkle leaf.
+4. Echo (send_echo_left, 413-425): validator j sends its shard and proof to
+   every node but its f right-hand neighbours.  Since every rank hosts
+   receivers, that fan-out is an all-gather of the validated rows: afterwards
+   every rank holds every row of every instance, [G][G*count][R][stride],
+   which is again a blocked layout -- decoded in place, no unpacking.
+5. every rank decodes every instance (compute_output -> decode_from_shards,
+   526-601) for the receivers it hosts.
 
-What is not re-run: the receiver's Proof::validate of each Echo (291)
-repeats step 3's computation on the same bytes, proof and index, and the
-other N-1 nodes' decodes reproduce the same payload from the same codeword;
-both are pure functions of identical inputs, so each is computed once.
-
-Layouts (row = one shard of `stride` bytes):
-  proposer slab   [count][G*R][stride]   rows >= N are padding (zeroed)
-  Value send/recv [G][count][R][stride]  block d of send = rows d*R.. of every
-                                         local instance; block s of recv =
-                                         this rank's rows of rank s's instances
-  Echo recv       [G][count][R][stride]  block v = rows v*R.. of every local
-                                         instance, as validated on rank v
-The regrouping is a plain strided copy done by torch (layout plumbing); every
-byte of shard, digest and payload data is computed by the HIP kernels.
+Per-GPU dedup (validate and decode are pure functions, so
+identical calls on one GPU are computed once; the bench reports faithful and
+executed counts):
+  * the receivers of rank g all decode the same codewords; the rank decodes
+    each instance once, as its first validator r0 = g*R sees it: every Echo
+    but those of r0's right-hand neighbours r0+1..r0+f (476-485), and none
+    from a validator whose Value failed (it sends no Echo, 254-256);
+  * rank g validates each Echo it receives once (291); rows of its own
+    validators were validated as their Values in step 3 (same bytes, proof,
+    index and root);
+  * the decode reuses those validations' leaf digests (hbrbc_decode_rows
+    known_leaves): only the rows reconstruct rebuilds are hashed again.
+With global-dedup instance mode (bench.py default) the unit of work is one
+decode per instance; here it is one decode per instance per rank, which is
+what a node of a G-GPU deployment must do.
 """
 import torch
 
@@ -58,6 +60,8 @@ class Topology:
         if (world - 1) * self.rpg >= n:
             raise ValueError("n=%d does not give every one of %d ranks a validator" % (n, world))
         self.npad = self.rpg * world
+        # rows_per_block of the slabs (0: plain shard-major layout)
+        self.rows_per_block = self.rpg if world > 1 else 0
 
     def validators(self, rank):
         return range(rank * self.rpg, min((rank + 1) * self.rpg, self.n))
@@ -70,28 +74,22 @@ class Topology:
         vs = self.validators(rank)
         return [vs[i % len(vs)] for i in range(count)]
 
-    def echo_received(self, proposers, device=None):
-        """[count, n] bool: the receiver p gets an Echo from every validator but
-        its f right-hand neighbours p+1..p+f (broadcast.rs:476-485)."""
-        p = torch.as_tensor(proposers, dtype=torch.int64, device=device).view(-1, 1)
-        j = torch.arange(self.n, dtype=torch.int64, device=device).view(1, -1)
-        d = (j - p) % self.n
-        return ~((d >= 1) & (d <= self.f))
+    def receiver(self, rank):
+        """The validator whose view rank `rank` decodes with (its first)."""
+        return rank * self.rpg
 
+    def receiver_present(self, rank):
+        """n flags: the Echoes receiver(rank) gets -- all but its f right-hand
+        neighbours r0+1..r0+f (broadcast.rs:476-485)."""
+        r0 = self.receiver(rank)
+        right = {(r0 + d) % self.n for d in range(1, self.f + 1)}
+        return [0 if j in right else 1 for j in range(self.n)]
 
-# ---------------------------------------------------------- layout helpers ---
-def pack_rows(slab, world, rpg, out):
-    """[count][world*rpg][...] -> [world][count][rpg][...] (destination-major)."""
-    count = slab.shape[0]
-    out.copy_(slab.view(count, world, rpg, *slab.shape[2:]).transpose(0, 1))
-    return out
-
-
-def unpack_rows(buf, out):
-    """[world][count][rpg][...] -> [count][world*rpg][...] (inverse of pack_rows)."""
-    world, count, rpg = buf.shape[:3]
-    out.view(count, world, rpg, *buf.shape[3:]).copy_(buf.transpose(0, 1))
-    return out
+    def echo_rows(self, rank):
+        """Rows rank `rank` validates as Echoes: received by its receiver and
+        sent by validators of other ranks."""
+        pres = self.receiver_present(rank)
+        return [j for j in range(self.n) if pres[j] and self.owner(j) != rank]
 
 
 # ---------------------------------------------------------------- exchange ---
@@ -111,8 +109,8 @@ class DistExchange:
 
     def all_to_all(self, out, inp, async_op=False):
         """out[s] on this rank = inp[rank] on rank s (dim 0 = ranks).  With
-        async_op (NCCL only) returns a handle; wait() makes torch's current
-        stream wait for it, so the copy overlaps whatever is queued meanwhile."""
+        async_op (NCCL only) returns a handle; wait() makes the current stream
+        wait for it."""
         assert out.shape[0] == self.world and inp.shape[0] == self.world
         if self.world == 1:
             if out.data_ptr() != inp.data_ptr():
@@ -127,45 +125,70 @@ class DistExchange:
                                            async_op=async_op and not self.staged)
 
     def all_gather(self, out, inp, async_op=False):
-        """out[s] = inp of rank s."""
+        """out[s] = inp of rank s (dim 0 of out = ranks, inp flat or not)."""
+        assert out.shape[0] == self.world and out.numel() == self.world * inp.numel()
         if self.world == 1:
-            out[0].copy_(inp)
+            if out.data_ptr() != inp.data_ptr():
+                out.view(-1).copy_(inp.reshape(-1))
             return None
         if self.staged:
             parts = [torch.empty_like(inp, device="cpu") for _ in range(self.world)]
             self.dist.all_gather(parts, inp.cpu(), group=self.group)
-            out.copy_(torch.stack(parts))
+            out.view(self.world, -1).copy_(torch.stack([p.reshape(-1) for p in parts]))
             return None
-        return self.dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group,
+        return self.dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=self.group,
                                                 async_op=async_op)
 
 
-def wait_all(handles):
-    for h in handles:
-        if h is not None:
-            h.wait()
-
-
 class SoloExchange:
-    """The exchange of a one-rank run (no process group): every collective is
-    the identity, and ShardedBroadcast aliases its buffers so nothing moves."""
+    """The exchange of a one-rank run (no process group): ShardedBroadcast
+    aliases its buffers, so nothing moves."""
 
-    world, rank = 1, 0
+    world, rank, staged = 1, 0, True
 
     def all_to_all(self, out, inp, async_op=False):
         if out.data_ptr() != inp.data_ptr():
             out.copy_(inp)
 
     def all_gather(self, out, inp, async_op=False):
-        out[0].copy_(inp)
+        if out.data_ptr() != inp.data_ptr():
+            out.view(-1).copy_(inp.reshape(-1))
 
 
-def loopback_all_to_all(outs, ins):
-    """The all-to-all of `len(ins)` virtual ranks living in one process:
-    outs[d][s] = ins[s][d]."""
-    for d, o in enumerate(outs):
-        for s, i in enumerate(ins):
-            o[s].copy_(i[d])
+class CommTimer:
+    """Collectives issued from a side stream, bracketed by timing events there.
+    The side stream first waits for the data (an event recorded on the
+    compute stream), so start -> end is the time the exchange occupies, also
+    when it overlaps compute of other sub-batches.  run() returns the event
+    the compute stream waits on before it reads the exchanged buffers."""
+
+    def __init__(self, device):
+        self.cs = torch.cuda.Stream(device)
+        self.spans = []
+        self.timing = False
+
+    def run(self, fn):
+        ready = torch.cuda.Event()
+        ready.record()
+        self.cs.wait_event(ready)
+        with torch.cuda.stream(self.cs):
+            a = torch.cuda.Event(enable_timing=True) if self.timing else None
+            if a is not None:
+                a.record()
+            for h in fn():
+                if h is not None:
+                    h.wait()
+            b = torch.cuda.Event(enable_timing=self.timing)
+            b.record()
+        if a is not None:
+            self.spans.append((a, b))
+        return b
+
+    def elapsed_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.spans)
+
+    def reset(self):
+        self.spans = []
 
 
 # --------------------------------------------------------------- one rank ---
@@ -173,7 +196,7 @@ class ShardedBroadcast:
     """The per-rank state of the validator-sharded simulation: `count` local
     proposals of `plen` bytes per step on `device`."""
 
-    def __init__(self, n, count, plen, rank, world, device=0):
+    def __init__(self, n, count, plen, rank, world, device=0, specialise=True):
         self.topo = t = Topology(n, world)
         self.rank, self.world, self.count, self.plen = rank, world, count, plen
         self.rb = rb = RbcBatch(n, t.f, device=device)
@@ -181,50 +204,76 @@ class ShardedBroadcast:
         self.device = dev
         self.S = S = shard_len(plen, rb.k)
         self.stride = stride = rb.stride_for(S)
-        ds = max(rb.dslots, 1)
+        self.ds = ds = max(rb.dslots, 1)
+        self.dsz = ds * 32 + 16                 # digests ++ ndig ++ pad per row
         G, R, C = world, t.rpg, count
+        self.rpb = t.rows_per_block
         u8 = dict(dtype=torch.uint8, device=dev)
         self.proposers = t.proposers(rank, C)
-        # proposer side
-        self.slab = torch.zeros((C, t.npad, stride), **u8)
+        # proposer side: destination-major slab [G][C][R][stride] (plain [C][n] at G=1)
+        self.slab = torch.zeros((G, C, R, stride), **u8)
         self.nodes = rb.alloc_nodes(C)
         self.digests = torch.zeros((C, n, ds, 32), **u8)
         self.ndig = torch.zeros((C, n), **u8)
-        # Value exchange (rows R per destination; G == 1 aliases, no copy)
-        if G == 1:
-            self.send_sh = self.slab.view(1, C, R, stride)
-        else:
-            self.send_sh = torch.empty((G, C, R, stride), **u8)
-        self.send_dg = torch.zeros((G, C, R, ds * 32 + 16), **u8)   # digests ++ ndig ++ pad
-        self.dg_flat = torch.zeros((C, t.npad, ds * 32 + 16), **u8)
-        self.recv_sh = self.send_sh if G == 1 else torch.empty_like(self.send_sh)
+        # Value exchange
+        self.dg_flat = torch.zeros((C, t.npad, self.dsz), **u8)
+        self.send_dg = torch.zeros((G, C, R, self.dsz), **u8)
+        self.recv_sh = self.slab if G == 1 else torch.empty_like(self.slab)
         self.recv_dg = self.send_dg if G == 1 else torch.empty_like(self.send_dg)
         self.roots_all = torch.empty((G, C, 32), **u8)
-        # validator side: the claimed/expected index of every received row
-        idx = torch.arange(rank * R, (rank + 1) * R, dtype=torch.int32, device=dev)
-        self.recv_idx = idx.view(1, 1, R).expand(G, C, R).contiguous()
-        self.ok_v = torch.zeros((G, C, R), **u8)
-        self.v_digests = torch.empty((G, C, R, ds, 32), **u8)
-        self.v_ndig = torch.empty((G, C, R), **u8)
-        # Echo exchange back to the proposer's rank
-        self.echo_sh = self.recv_sh if G == 1 else torch.empty_like(self.recv_sh)
-        self.echo_ok = self.ok_v if G == 1 else torch.empty_like(self.ok_v)
-        # receiver side
-        self.dec_slab = self.slab if G == 1 else torch.zeros((C, t.npad, stride), **u8)
-        self.echo_mask = t.echo_received(self.proposers, device=dev).to(torch.uint8)
-        self.present = torch.empty((C, n), **u8)
-        self.nodes2 = rb.alloc_nodes(C)
-        self.out = torch.zeros((C, max(16, (rb.k * S + 15) // 16 * 16)), **u8)
-        self.plen_out = torch.zeros(C, dtype=torch.int32, device=dev)
-        self.status = torch.zeros(C, dtype=torch.int32, device=dev)
-        rb.reserve(C)
+        # validator side: Value proofs of this rank's rows of every instance
+        self.vreal = len(t.validators(rank))
+        self.vrows_t = torch.arange(self.vreal, dtype=torch.int32, device=dev)
+        idx = torch.arange(rank * R, rank * R + self.vreal, dtype=torch.int32, device=dev)
+        self.recv_idx = idx.view(1, self.vreal).expand(G * C, self.vreal).contiguous()
+        self.ok_v = torch.zeros((G * C, self.vreal), **u8)
+        self.v_digests = torch.zeros((G * C, R, ds, 32), **u8)
+        self.v_ndig = torch.zeros((G * C, R), **u8)
+        # Echo all-gather: every row of every instance, [G_v][G*C][R][stride]
+        self.echo_sh = self.recv_sh if G == 1 else torch.empty((G, G * C, R, stride), **u8)
+        self.echo_dg = self.recv_dg if G == 1 else torch.empty((G, G * C, R, self.dsz), **u8)
+        self.e_digests = self.digests if G == 1 else torch.zeros((G * C, t.npad, ds, 32), **u8)
+        self.e_ndig = self.ndig if G == 1 else torch.zeros((G * C, t.npad), **u8)
+        self.echo_rows = t.echo_rows(rank) if G > 1 else []
+        self.echo_rows_t = torch.tensor(self.echo_rows or [0], dtype=torch.int32, device=dev)
+        self.ok_e = torch.zeros((G * C, max(1, len(self.echo_rows))), **u8)
+        # receiver side: decode of every instance of every rank
+        pres = t.receiver_present(rank)
+        self.pattern = pres
+        own = [j for j in t.validators(rank) if pres[j]]
+        self.own_present = own
+        self.present = torch.zeros((G * C, n), **u8)
+        self.dec_nodes = rb.alloc_nodes(G * C)
+        self.out = torch.zeros((G * C, max(16, (rb.k * S + 15) // 16 * 16)), **u8)
+        self.plen_out = torch.zeros(G * C, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(G * C, dtype=torch.int32, device=dev)
+        self.own_cols = torch.tensor([j - rank * R for j in own] or [0], dtype=torch.int64,
+                                     device=dev)
+        self.own_rows = torch.tensor(own or [0], dtype=torch.int64, device=dev)
+        self.echo_cols = torch.tensor(self.echo_rows or [0], dtype=torch.int64, device=dev)
+        rb.reserve(G * C)
+        if specialise:
+            rb.specialise_decoder(pres, self.rpb)
+
+    # layouts: (shard_stride, rows_per_block, block_stride, inst_stride) --------
+    def _prop_layout(self):
+        G, R, C, st = self.world, self.topo.rpg, self.count, self.stride
+        if G == 1:
+            return st, 0, 0, self.topo.n * st
+        return st, R, C * R * st, R * st
+
+    def _echo_layout(self):
+        G, R, C, st = self.world, self.topo.rpg, self.count, self.stride
+        if G == 1:
+            return st, 0, 0, self.topo.n * st
+        return st, R, G * C * R * st, R * st
 
     # 1. proposer: frame, encode, tree, proofs -------------------------------
     def propose(self, payloads):
-        rb, S = self.rb, self.S
-        slab = self.slab[:, : self.topo.n]
-        rb.frame_encode(payloads, self.plen, slab)
-        rb.merkle(slab, S, self.nodes)
+        rb, S, C, n = self.rb, self.S, self.count, self.topo.n
+        st, rpb, bst, ist = self._prop_layout()
+        rb.frame_encode_rows(payloads, self.plen, self.slab, C, st, rpb, bst, ist)
+        rb.merkle_rows(self.slab, S, C, st, rpb, bst, ist, self.nodes)
         rb.proofs(self.nodes, self.digests, self.ndig)
 
     def roots(self):
@@ -232,48 +281,77 @@ class ShardedBroadcast:
 
     # 2. Value messages ---------------------------------------------------------
     def pack_value(self):
-        G, R, C = self.world, self.topo.rpg, self.count
-        n, ds = self.topo.n, self.digests.shape[2]
-        if G > 1:
-            pack_rows(self.slab, G, R, self.send_sh)
-        flat = self.dg_flat
-        flat[:, :n, : ds * 32] = self.digests.view(C, n, ds * 32)
-        flat[:, :n, ds * 32] = self.ndig
-        pack_rows(flat, G, R, self.send_dg)
+        """Digests (+ their counts) regrouped destination-major next to the
+        slab, which the encoder already wrote that way (metadata only)."""
+        if self.world == 1:
+            return
+        G, R, C, ds, n = self.world, self.topo.rpg, self.count, self.ds, self.topo.n
+        self.dg_flat[:, :n, : ds * 32].copy_(self.digests.view(C, n, ds * 32))
+        self.dg_flat[:, :n, ds * 32].copy_(self.ndig)
+        self.send_dg.copy_(self.dg_flat.view(C, G, R, self.dsz).transpose(0, 1))
 
     def exchange_value(self, ex, async_op=False):
         """Value messages (+ the roots' all-gather); returns the handles."""
         self._roots = self.roots().contiguous()   # kept alive while in flight
-        return [ex.all_to_all(self.recv_sh, self.send_sh, async_op),
+        if self.world == 1:
+            self.roots_all[0].copy_(self._roots)
+            return []
+        return [ex.all_to_all(self.recv_sh, self.slab, async_op),
                 ex.all_to_all(self.recv_dg, self.send_dg, async_op),
                 ex.all_gather(self.roots_all, self._roots, async_op)]
 
     # 3. validators validate their Values --------------------------------------
     def validate_values(self):
-        G, R, C = self.world, self.topo.rpg, self.count
-        ds = self.digests.shape[2]
-        self.v_digests.view(G, C, R, ds * 32).copy_(self.recv_dg[..., : ds * 32])
-        self.v_ndig.copy_(self.recv_dg[..., ds * 32])
-        self.rb.validate_rows(self.recv_sh.view(G * C, R, self.stride), self.S, R,
-                              self.recv_idx.view(G * C, R), self.v_digests.view(G * C, R, ds, 32),
-                              self.v_ndig.view(G * C, R), self.roots_all.view(G * C, 32),
-                              self.ok_v.view(G * C, R))
+        G, R, C, ds, n = self.world, self.topo.rpg, self.count, self.ds, self.topo.n
+        if G == 1:
+            dig, nd, drows, ist = self.digests, self.ndig, n, n * self.stride
+        else:
+            src = self.recv_dg.view(G * C, R, self.dsz)
+            self.v_digests.view(G * C, R, ds * 32).copy_(src[..., : ds * 32])
+            self.v_ndig.copy_(src[..., ds * 32])
+            dig, nd, drows, ist = self.v_digests, self.v_ndig, R, R * self.stride
+        # this rank's rows of every instance, [G*C][R][stride]; their leaves go
+        # to level 0 of the decode trees at index rank*R + r
+        self.rb.validate_layout(self.recv_sh, self.S, G * C, self.vreal, self.stride, 0, 0, ist,
+                                dig, nd, drows, self.roots_all.view(G * C, 32), self.ok_v,
+                                rows=self.vrows_t, indices=self.recv_idx,
+                                leaf_out=self.dec_nodes[:, self.rank * R:])
 
-    # 4. Echo messages back to the proposer's rank ------------------------------
+    # 4. Echo messages: all-gather of the validated rows ------------------------
     def exchange_echo(self, ex, async_op=False):
-        """Echo messages back to the proposers' ranks; returns the handles."""
-        return [ex.all_to_all(self.echo_sh, self.recv_sh, async_op),
-                ex.all_to_all(self.echo_ok, self.ok_v, async_op)]
+        if self.world == 1:
+            return []
+        return [ex.all_gather(self.echo_sh, self.recv_sh, async_op),
+                ex.all_gather(self.echo_dg, self.recv_dg, async_op)]
 
-    # 5. the receiver decodes ---------------------------------------------------
+    def validate_echoes(self):
+        """Proof::validate of every Echo the receiver gets from other ranks'
+        validators (handle_echo, broadcast.rs:291); the leaves go to the
+        decode trees."""
+        G, R, C, ds = self.world, self.topo.rpg, self.count, self.ds
+        if G == 1 or not self.echo_rows:
+            return
+        # digests of every row of every instance in the validate layout [G*C][npad]
+        src = self.echo_dg.view(G, G * C, R, self.dsz)
+        self.e_digests.view(G * C, G, R, ds * 32).copy_(src[..., : ds * 32].transpose(0, 1))
+        self.e_ndig.view(G * C, G, R).copy_(src[..., ds * 32].transpose(0, 1))
+        st, rpb, bst, ist = self._echo_layout()
+        self.rb.validate_layout(self.echo_sh, self.S, G * C, len(self.echo_rows), st, rpb, bst,
+                                ist, self.e_digests, self.e_ndig, self.topo.npad,
+                                self.roots_all.view(G * C, 32), self.ok_e,
+                                rows=self.echo_rows_t, leaf_out=self.dec_nodes)
+
+    # 5. every rank decodes every instance ------------------------------------
     def decode(self):
-        G, n = self.world, self.topo.n
-        if G > 1:
-            unpack_rows(self.echo_sh, self.dec_slab)
-        ok = self.echo_ok.transpose(0, 1).reshape(self.count, self.topo.npad)[:, :n]
-        torch.mul(ok, self.echo_mask, out=self.present)
-        self.rb.decode(self.dec_slab[:, :n], self.S, self.present, self.roots(), self.nodes2,
-                       self.out, self.plen_out, self.status)
+        self.present.zero_()
+        if self.own_present:
+            self.present[:, self.own_rows] = self.ok_v[:, self.own_cols]
+        if self.echo_rows:
+            self.present[:, self.echo_cols] = self.ok_e[:, : len(self.echo_rows)]
+        st, rpb, bst, ist = self._echo_layout()
+        self.rb.decode_rows(self.echo_sh, self.S, self.world * self.count, st, rpb, bst, ist,
+                            self.present, self.roots_all.view(-1, 32), self.dec_nodes, self.out,
+                            self.plen_out, self.status, known_leaves=True)
 
     def step(self, payloads, ex):
         self.propose(payloads)
@@ -281,26 +359,45 @@ class ShardedBroadcast:
         self.exchange_value(ex)
         self.validate_values()
         self.exchange_echo(ex)
+        self.validate_echoes()
         self.decode()
 
+    # accounting --------------------------------------------------------------
+    def counts(self):
+        """Per-step work of this rank: executed (per-GPU dedup) and faithful
+        (every receiver of this rank's block, as the reference runs them)."""
+        t, inst = self.topo, self.world * self.count
+        present = sum(self.pattern)
+        return {
+            "value_validates": inst * self.vreal,
+            "echo_validates": inst * len(self.echo_rows),
+            "decodes": inst,
+            "decode_leaf_hashes": inst * (t.n - present),
+            "faithful_value_validates": inst * self.vreal,
+            "faithful_echo_validates": inst * self.vreal * (t.n - t.f),
+            "faithful_decodes": inst * self.vreal,
+            "faithful_decode_leaf_hashes": inst * self.vreal * t.n,
+        }
 
-def pipelined_step(subs, payloads, ex):
+
+def pipelined_step(subs, payloads, ex, timer):
     """One step over several sub-batches (ShardedBroadcast objects on the same
-    rank, payloads[i] for subs[i]) with every exchange in flight while the next
-    sub-batch computes: propose all -> (Value of i overlaps propose of i+1) ->
-    validate i while Value i+1 / Echo i-1 move -> decode i while Echo i+1
-    moves.  With NCCL the collectives run on the communicator's stream and
-    handle.wait() only orders torch's current stream after them."""
+    rank, payloads[i] for subs[i]) with every exchange in flight on the
+    timer's side stream while the compute stream works on other sub-batches:
+    propose all -> (Value of i overlaps propose of i+1) -> validate i while
+    Value i+1 / Echo i-1 move -> decode i while Echo i+1 moves."""
     n = len(subs)
-    hv, he = [None] * n, [None] * n
+    ev_v, ev_e = [None] * n, [None] * n
+    cur = torch.cuda.current_stream()
     for i, sb in enumerate(subs):
         sb.propose(payloads[i])
         sb.pack_value()
-        hv[i] = sb.exchange_value(ex, async_op=True)
+        ev_v[i] = timer.run(lambda sb=sb: sb.exchange_value(ex, async_op=True))
     for i, sb in enumerate(subs):
-        wait_all(hv[i])
+        cur.wait_event(ev_v[i])
         sb.validate_values()
-        he[i] = sb.exchange_echo(ex, async_op=True)
+        ev_e[i] = timer.run(lambda sb=sb: sb.exchange_echo(ex, async_op=True))
     for i, sb in enumerate(subs):
-        wait_all(he[i])
+        cur.wait_event(ev_e[i])
+        sb.validate_echoes()
         sb.decode()

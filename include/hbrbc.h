@@ -192,14 +192,85 @@ int hbrbc_reconstruct_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len,
  * hold that many bytes, bytes past the payload are written 0), their length to payload_len_out[i] and
  * the outcome to status_out[i] (OK, TOO_FEW_SHARDS_PRESENT, ROOT_MISMATCH,
  * NO_PAYLOAD_LEN).  `nodes` (count x node_inst_stride) receives the
- * re-built trees. */
+ * re-built trees.  Every byte of every instance's payload row up to
+ * round_up(data*shard_len - 4, 16) is written: past the payload (all of it
+ * for a failed instance) with 0. */
 int hbrbc_decode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t shard_stride,
                        size_t inst_stride, const uint8_t *present, size_t count,
                        const uint8_t *roots, size_t root_stride, uint8_t *nodes,
                        size_t node_inst_stride, uint8_t *payload_out, size_t payload_stride,
                        uint32_t *payload_len_out, int32_t *status_out, void *stream);
-/* Pre-size the reconstruct workspace for `count` instances. */
+/* Pre-size the reconstruct workspace (and the decode-matrix cache) for
+ * `count` instances; growing it empties the cache. */
 int hbrbc_reserve(hbrbc_ctx *ctx, size_t count);
+
+/* ---- blocked row layouts (validator-sharded slabs) ----------------------- */
+/* The *_rows variants take the same arguments as their *_batch forms plus a
+ * row placement: row j of instance i lives at
+ *   base + i*inst_stride + (j / rows_per_block)*block_stride
+ *        + (j % rows_per_block)*shard_stride
+ * rows_per_block == 0 or >= n is the plain layout above (row j at
+ * j*shard_stride).  With rows_per_block < n (<= 255): inst_stride >=
+ * rows_per_block*shard_stride and block_stride >= count*inst_stride, e.g.
+ * the destination-major Value slab [rank][instance][rows_per_block][stride]
+ * whose block d is the contiguous chunk an all-to-all sends to rank d, or the
+ * Echo all-gather [validator rank][instance][rows_per_block][stride]. */
+int hbrbc_frame_encode_rows(hbrbc_ctx *ctx, const uint8_t *payloads, size_t payload_stride,
+                            size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
+                            size_t shard_stride, size_t rows_per_block, size_t block_stride,
+                            size_t inst_stride, void *stream);
+int hbrbc_merkle_rows(hbrbc_ctx *ctx, const uint8_t *shards, size_t shard_len, size_t shard_stride,
+                      size_t rows_per_block, size_t block_stride, size_t inst_stride, size_t count,
+                      uint8_t *nodes, size_t node_inst_stride, void *stream);
+/* Proof::validate (merkle.rs:83-103) for `count` x `per_inst` proofs: proof
+ * (i, jj) checks value row r = rows[jj] (rows: device uint32[per_inst], the
+ * same for every instance; NULL: r = jj) of instance i in the row layout
+ * above, with claimed index indices[i*per_inst + jj] (NULL: r), digests and
+ * ndig of proof slot i*digest_rows + r (rows given; every r < digest_rows) or
+ * i*per_inst + jj, against roots + i*root_stride.  ok_out[i*per_inst + jj].
+ * leaf_out (optional): SHA3-256 of the value -- the Merkle leaf -- to
+ * leaf_out + i*leaf_inst_stride + r*32, e.g. level 0 of a node slab that a
+ * later hbrbc_decode_rows(known_leaves = 1) completes. */
+int hbrbc_validate_rows(hbrbc_ctx *ctx, const uint8_t *values, size_t value_len,
+                        size_t value_stride, size_t rows_per_block, size_t block_stride,
+                        size_t value_inst_stride, size_t per_inst, const uint32_t *rows,
+                        const uint32_t *indices, const uint8_t *digests, const uint8_t *ndig,
+                        size_t digest_rows, const uint8_t *roots, size_t root_stride,
+                        size_t tree_n, size_t count, uint8_t *ok_out, uint8_t *leaf_out,
+                        size_t leaf_inst_stride, void *stream);
+int hbrbc_reconstruct_rows(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                           size_t rows_per_block, size_t block_stride, size_t inst_stride,
+                           const uint8_t *present, size_t count, int32_t *status_out,
+                           void *stream);
+/* decode_from_shards in the row layout above.  known_leaves != 0: level 0 of
+ * `nodes` already holds SHA3-256 of every PRESENT row of every instance (the
+ * receiver hashed them when it validated their Echo proofs, broadcast.rs:291,
+ * e.g. through hbrbc_validate_rows' leaf_out); only the rows reconstruct
+ * rebuilds are hashed before the levels, root compare and unframe. */
+int hbrbc_decode_rows(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t shard_stride,
+                      size_t rows_per_block, size_t block_stride, size_t inst_stride,
+                      const uint8_t *present, size_t count, const uint8_t *roots,
+                      size_t root_stride, uint8_t *nodes, size_t node_inst_stride,
+                      int known_leaves, uint8_t *payload_out, size_t payload_stride,
+                      uint32_t *payload_len_out, int32_t *status_out, void *stream);
+
+/* ---- decode-matrix cache (rse's per-pattern decode-matrix LRU) ----------- */
+/* Every reconstruct/decode call looks each instance's present pattern up in a
+ * device hash table: the first instance of a new pattern computes inv(M[first
+ * k present]) and the recovery rows into a shared slot, every other instance
+ * of that pattern -- in this call or a later one -- reuses them.  Shared
+ * slots are flushed after about 4 x capacity insertions.  Calls on one
+ * context must be stream-ordered (the cache is context state). */
+int hbrbc_decode_cache_clear(hbrbc_ctx *ctx);
+/* Shared slots claimed since the last flush (synchronises the device). */
+int hbrbc_decode_cache_fill(hbrbc_ctx *ctx, uint32_t *patterns_out);
+/* Pattern-specialised decoder: compile (hiprtc; or load from the code-object
+ * cache) an XOR network for the erasure pattern `present` (host, n bytes)
+ * in layouts with this rows_per_block (0: plain).  Later reconstruct/decode
+ * calls in that layout run it for every instance of the pattern and the
+ * generic kernel for the rest; one pattern per layout (a new call replaces
+ * the previous one).  HBRBC_JIT=0 forbids compiling (cache only). */
+int hbrbc_decoder_specialise(hbrbc_ctx *ctx, const uint8_t *present, size_t rows_per_block);
 
 /* ---- wire format: bincode of broadcast::Message -------------------------- */
 /* `Message::{Value, Echo}(Proof<Vec<u8>>)` (message.rs:13-24, merkle.rs:72-78) as
@@ -240,7 +311,7 @@ int hbrbc_wire_decode_batch(hbrbc_ctx *ctx, const uint8_t *msgs, size_t msg_stri
  * object for this (data, parity) matrix is cached under <lib dir>/jit (or
  * $HBRBC_JIT_DIR), a kernel generated for the matrix: a fixed XOR network on
  * bit planes (hbbft_amd/csrc/jit.hip), bit-identical output.  Returns
- * "specialised", "bitslice", "perm", "trivial" or "jit-failed". */
+ * "specialised", "bitslice", "trivial" or "jit-failed". */
 const char *hbrbc_encode_kernel(const hbrbc_ctx *ctx);
 /* Generate and compile (hiprtc, gfx950, no device needed) the specialised
  * encoder for rse build_matrix(data, data + parity) into `dir` (NULL: the
@@ -257,6 +328,18 @@ int hbrbc_jit_build_encode_group(size_t data_shards, size_t parity_shards, size_
  * current generator settings; 0 and a NUL-terminated name in buf, or an error. */
 int hbrbc_jit_file_name(size_t data_shards, size_t parity_shards, size_t group, char *buf,
                         size_t buf_len);
+/* The same for the encoder of a blocked row layout (rows_per_block < n). */
+int hbrbc_jit_build_encode_rows(size_t data_shards, size_t parity_shards, size_t group,
+                                size_t rows_per_block, const char *dir);
+int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t group,
+                               size_t rows_per_block, char *buf, size_t buf_len);
+/* Pattern-specialised decoders (hbrbc_decoder_specialise) built ahead of use:
+ * groups of the pattern's program, one group's code object, its file name. */
+size_t hbrbc_jit_decode_groups(size_t data_shards, size_t parity_shards, const uint8_t *present);
+int hbrbc_jit_build_decode(size_t data_shards, size_t parity_shards, const uint8_t *present,
+                           size_t rows_per_block, size_t group, const char *dir);
+int hbrbc_jit_decode_file_name(size_t data_shards, size_t parity_shards, const uint8_t *present,
+                               size_t rows_per_block, size_t group, char *buf, size_t buf_len);
 
 /* ---- measurement hooks (bench.py) --------------------------------------- */
 /* Stage ids for the per-stage device timers. */

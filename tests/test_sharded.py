@@ -1,10 +1,11 @@
 """Validator-sharded simulation (hbbft_amd/sharded.py).
 
-CPU (gloo, world 2): the topology, the destination-major regrouping and the
-two all-to-alls move every shard row to the rank hosting its validator and
-back.  GPU: G virtual ranks in one process (loopback exchange) run the whole
-step through libhbrbc.so and are checked against the oracle; a 2-rank gloo
-run shares cuda:0."""
+CPU (gloo, world 2 and 3): the topology, and that the Value all-to-all of a
+destination-major slab followed by the Echo all-gather leaves every rank with
+every row of every instance in the blocked layout the decoder reads.
+GPU: G virtual ranks in one process (loopback exchange) run the whole step
+through libhbrbc.so and are checked against the oracle; a 2-rank gloo run
+shares cuda:0 (step and pipelined schedule)."""
 import os
 import socket
 
@@ -12,8 +13,8 @@ import numpy as np
 import pytest
 import torch
 
-from hbbft_amd.sharded import (DistExchange, ShardedBroadcast, SoloExchange, Topology,
-                               loopback_all_to_all, pack_rows, pipelined_step, unpack_rows)
+from hbbft_amd.sharded import (CommTimer, DistExchange, ShardedBroadcast, SoloExchange, Topology,
+                               pipelined_step)
 from oracle import pyoracle as orc
 
 
@@ -28,27 +29,25 @@ def free_port():
 # ------------------------------------------------------------------ CPU ----
 def test_topology():
     t = Topology(10, 4)
-    assert t.rpg == 3 and t.npad == 12
+    assert t.rpg == 3 and t.npad == 12 and t.rows_per_block == 3
     assert [list(t.validators(r)) for r in range(4)] == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9]]
     assert t.proposers(3, 3) == [9, 9, 9] and t.proposers(1, 4) == [3, 4, 5, 3]
     with pytest.raises(ValueError):
         Topology(9, 4)   # the last rank would host no validator
-    # receiver p misses Echoes from p+1..p+f (broadcast.rs:476-485), f = 3
-    m = t.echo_received([0, 8]).numpy()
-    assert m[0].tolist() == [1, 0, 0, 0, 1, 1, 1, 1, 1, 1]
-    assert m[1].tolist() == [0, 0, 1, 1, 1, 1, 1, 1, 1, 0]   # 9, 0, 1 wrap around
-    assert m.sum(axis=1).tolist() == [7, 7]
+    # receiver r0 = g*R misses Echoes from r0+1..r0+f (broadcast.rs:476-485), f = 3
+    assert [t.receiver(r) for r in range(4)] == [0, 3, 6, 9]
+    assert t.receiver_present(0) == [1, 0, 0, 0, 1, 1, 1, 1, 1, 1]
+    assert t.receiver_present(3) == [0, 0, 0, 1, 1, 1, 1, 1, 1, 1]   # 10, 11, 12 wrap to 0, 1, 2
+    assert all(sum(t.receiver_present(r)) == 10 - 3 for r in range(4))
+    # Echo rows: received and from other ranks' validators
+    assert t.echo_rows(0) == [4, 5, 6, 7, 8, 9]
+    assert t.echo_rows(3) == [3, 4, 5, 6, 7, 8]
+    assert Topology(64, 1).rows_per_block == 0 and Topology(64, 8).rows_per_block == 8
 
 
-def test_pack_unpack_roundtrip():
-    g = torch.Generator().manual_seed(1)
-    slab = torch.randint(0, 256, (5, 12, 48), dtype=torch.uint8, generator=g)
-    buf = torch.empty((4, 5, 3, 48), dtype=torch.uint8)
-    pack_rows(slab, 4, 3, buf)
-    for d in range(4):
-        assert torch.equal(buf[d], slab[:, 3 * d: 3 * d + 3])
-    back = torch.empty_like(slab)
-    assert torch.equal(unpack_rows(buf, back), slab)
+def blocked_row(buf, j, t, R, stride):
+    """Row j of instance t of a blocked slab [blocks][instances][R][stride]."""
+    return buf[j // R, t, j % R, :stride]
 
 
 def _gloo_worker(rank, world, port, n, count, plen, q):
@@ -57,32 +56,41 @@ def _gloo_worker(rank, world, port, n, count, plen, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         t = Topology(n, world)
+        R = t.rpg
         ex = DistExchange()
         f = t.f
         S = orc.shard_len(plen, n - 2 * f)
 
-        def slab_of(r):   # what rank r's proposer side holds (oracle shards)
-            out = torch.zeros((count, t.npad, S), dtype=torch.uint8)
-            for i in range(count):
-                sh, _ = orc.send_shards(n, f, orc.gen_payload(100 + r, i, plen).tobytes())
-                out[i, :n] = torch.from_numpy(sh)
-            return out
+        def shards_of(r, i):
+            sh, _ = orc.send_shards(n, f, orc.gen_payload(100 + r, i, plen).tobytes())
+            return torch.from_numpy(sh)
 
-        mine = slab_of(rank)
-        send = pack_rows(mine, world, t.rpg, torch.empty((world, count, t.rpg, S), dtype=torch.uint8))
-        recv = torch.empty_like(send)
-        ex.all_to_all(recv, send)
+        # what the encoder writes: the destination-major slab [G][C][R][S]
+        slab = torch.zeros((world, count, R, S), dtype=torch.uint8)
+        for i in range(count):
+            sh = shards_of(rank, i)
+            for j in range(n):
+                slab[j // R, i, j % R] = sh[j]
+        recv = torch.empty_like(slab)
+        ex.all_to_all(recv, slab)
         # Value: block s = this rank's validators' rows of rank s's instances
         for s in range(world):
-            assert torch.equal(recv[s], slab_of(s)[:, rank * t.rpg:(rank + 1) * t.rpg])
+            for i in range(count):
+                sh = shards_of(s, i)
+                for r in range(len(t.validators(rank))):
+                    assert torch.equal(recv[s, i, r], sh[rank * R + r])
         roots = torch.full((count, 32), rank, dtype=torch.uint8)
         allr = torch.empty((world, count, 32), dtype=torch.uint8)
         ex.all_gather(allr, roots)
         assert [int(allr[s, 0, 0]) for s in range(world)] == list(range(world))
-        # Echo back to the proposer's rank, then regroup = the original slab
-        echo = torch.empty_like(recv)
-        ex.all_to_all(echo, recv)
-        assert torch.equal(unpack_rows(echo, torch.empty_like(mine)), mine)
+        # Echo all-gather: [G_v][G*C][R][S]; instance (s, i) = s*C + i, row j in block j // R
+        echo = torch.empty((world, world * count, R, S), dtype=torch.uint8)
+        ex.all_gather(echo, recv)
+        for s in range(world):
+            for i in range(count):
+                sh = shards_of(s, i)
+                for j in range(n):
+                    assert torch.equal(blocked_row(echo, j, s * count + i, R, S), sh[j])
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))
@@ -91,7 +99,7 @@ def _gloo_worker(rank, world, port, n, count, plen, q):
 
 
 @pytest.mark.parametrize("n,world", [(10, 2), (16, 2), (7, 3)])
-def test_gloo_value_and_echo_exchange(n, world):
+def test_gloo_value_all_to_all_and_echo_all_gather(n, world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -114,26 +122,36 @@ def _payloads(seed, count, plen, dev):
     return pay, t
 
 
-def run_loopback(n, world, count, plen, tamper=None):
-    ranks = [ShardedBroadcast(n, count, plen, r, world, device=0) for r in range(world)]
+def run_loopback(n, world, count, plen, tamper=None, specialise=True):
+    """One step of `world` virtual ranks in this process; the collectives are
+    the loopback copies an all-to-all / all-gather would make."""
+    ranks = [ShardedBroadcast(n, count, plen, r, world, device=0, specialise=specialise)
+             for r in range(world)]
     pays = []
     for r, sb in enumerate(ranks):
         pay, t = _payloads(500 + r, count, plen, sb.device)
         pays.append(pay)
         sb.propose(t)
         sb.pack_value()
-    loopback_all_to_all([sb.recv_sh for sb in ranks], [sb.send_sh for sb in ranks])
-    loopback_all_to_all([sb.recv_dg for sb in ranks], [sb.send_dg for sb in ranks])
-    for sb in ranks:
-        for s, src in enumerate(ranks):
-            sb.roots_all[s].copy_(src.roots())
+    if world == 1:
+        ranks[0].exchange_value(SoloExchange())
+    else:
+        for d, dst in enumerate(ranks):           # Value all-to-all
+            for s, src in enumerate(ranks):
+                dst.recv_sh[s].copy_(src.slab[d])
+                dst.recv_dg[s].copy_(src.send_dg[d])
+                dst.roots_all[s].copy_(src.roots())
     if tamper:
         tamper(ranks)
     for sb in ranks:
         sb.validate_values()
-    loopback_all_to_all([sb.echo_sh for sb in ranks], [sb.recv_sh for sb in ranks])
-    loopback_all_to_all([sb.echo_ok for sb in ranks], [sb.ok_v for sb in ranks])
+    if world > 1:
+        for dst in ranks:                         # Echo all-gather
+            for v, src in enumerate(ranks):
+                dst.echo_sh[v].copy_(src.recv_sh.view(dst.echo_sh[v].shape))
+                dst.echo_dg[v].copy_(src.recv_dg.view(dst.echo_dg[v].shape))
     for sb in ranks:
+        sb.validate_echoes()
         sb.decode()
     torch.cuda.synchronize()
     return ranks, pays
@@ -141,54 +159,76 @@ def run_loopback(n, world, count, plen, tamper=None):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,world,count,plen", [(16, 2, 3, 5000), (10, 4, 2, 777), (64, 8, 2, 20000),
-                                                (7, 3, 4, 100), (128, 4, 2, 6000)])
+                                                (7, 3, 4, 100), (128, 4, 2, 6000), (64, 1, 3, 9000)])
 def test_sharded_loopback_vs_oracle(n, world, count, plen):
     ranks, pays = run_loopback(n, world, count, plen)
     t = ranks[0].topo
+    R = t.rpg
     for r, sb in enumerate(ranks):
         S = sb.S
-        slab = sb.slab.cpu().numpy()
+        slab = sb.slab.cpu()
         nodes = sb.nodes.cpu().numpy()
         for i in range(count):
             sh, nd = orc.send_shards(n, t.f, pays[r][i].tobytes())
-            assert np.array_equal(slab[i, :n, :S], sh)
+            for j in range(n):   # the encoder wrote the destination-major slab
+                row = blocked_row(slab, j, i, R, S) if world > 1 else slab[0, i, j, :S]
+                assert np.array_equal(row.numpy(), sh[j]), (r, i, j)
             assert np.array_equal(nodes[i], nd)
-        # every real row this rank validated is valid
-        ok = sb.ok_v.cpu().numpy()
-        real = len(t.validators(r))
-        assert ok[:, :, :real].all()
-        # the receiver saw exactly N - f Echoes and decoded every payload
+        assert sb.ok_v.cpu().numpy().all()             # every Value validates
+        if sb.echo_rows:
+            assert sb.ok_e.cpu().numpy()[:, : len(sb.echo_rows)].all()
+        # the receiver saw exactly N - f Echoes and decoded every payload of every rank
         assert (sb.present.cpu().numpy().sum(axis=1) == n - t.f).all()
         assert (sb.status.cpu().numpy() == 0).all()
         assert (sb.plen_out.cpu().numpy() == plen).all()
-        assert np.array_equal(sb.out.cpu().numpy()[:, :plen], pays[r])
-        assert np.array_equal(sb.nodes2.cpu().numpy(), nodes)
+        out = sb.out.cpu().numpy()
+        dn = sb.dec_nodes.cpu().numpy()
+        for s in range(world):
+            for i in range(count):
+                assert np.array_equal(out[s * count + i, :plen], pays[s][i])
+                # the decode tree (reused leaves + rebuilt rows) is the proposer's tree
+                assert np.array_equal(dn[s * count + i], ranks[s].nodes[i].cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_sharded_generic_decoder_matches_specialised():
+    """The pattern-specialised decoder and the generic kernel give the same bytes."""
+    a, pa = run_loopback(16, 2, 2, 3000, specialise=True)
+    b, pb = run_loopback(16, 2, 2, 3000, specialise=False)
+    for x, y in zip(a, b):
+        assert torch.equal(x.echo_sh, y.echo_sh)
+        assert torch.equal(x.out, y.out)
 
 
 @pytest.mark.gpu
 def test_sharded_faulty_rows():
     """A shard corrupted in transit fails its Value validation, so that
-    validator sends no Echo; the receiver still decodes from the rest, and
-    with more than f missing it reports TooFewShardsPresent."""
+    validator sends no Echo (broadcast.rs:254-256) and every receiver's Echo
+    validation of it fails too; receivers still decode from the rest, and with
+    too few rows left report TooFewShardsPresent."""
     n, world, count, plen = 16, 2, 2, 3000
-    f = (n - 1) // 3
+    f = (n - 1) // 3   # 5; receivers 0 and 8 miss 1..5 and 9..13
 
     def tamper(ranks):
-        # rank 0 hosts validators 0..7; instance 0 of rank 1 (proposer 8):
-        # corrupt validator 0's row -> 1 more missing row (f + 1 total)
-        ranks[0].recv_sh[1, 0, 0, 5] ^= 0x40
-        # instance 1 of rank 1 (proposer 9): corrupt f + 1 more rows -> too few
-        for r in range(f + 1):
+        # instance 0 of rank 1: validator 6 (rank 0) gets a corrupted row
+        ranks[0].recv_sh[1, 0, 6, 5] ^= 0x40
+        # instance 1 of rank 1: validators 0..7 all corrupted -> receiver 8 keeps 3 < k = 6
+        for r in range(8):
             ranks[0].recv_sh[1, 1, r, 0] ^= 1
 
     ranks, pays = run_loopback(n, world, count, plen, tamper)
-    ok = ranks[0].ok_v.cpu().numpy()
-    assert ok[1, 0, 0] == 0 and ok[1, 0, 1:].all()
-    assert not ok[1, 1, : f + 1].any()
-    st = ranks[1].status.cpu().numpy()
-    assert st[0] == 0 and st[1] == 10
-    assert np.array_equal(ranks[1].out.cpu().numpy()[0, :plen], pays[1][0])
-    assert (ranks[0].status.cpu().numpy() == 0).all()
+    ok = ranks[0].ok_v.cpu().numpy()          # [G*C][R]: instance (1, i) = row 2 + i
+    assert ok[2, 6] == 0 and ok[2, :6].all() and ok[2, 7]
+    assert not ok[3].any()
+    for sb in ranks:
+        pres = sb.present.cpu().numpy()
+        assert pres[2, 6] == 0
+    st0, st1 = ranks[0].status.cpu().numpy(), ranks[1].status.cpu().numpy()
+    assert (st0 == 0).all()                   # receiver 0 keeps rows 8..15 of instance (1, 1)
+    assert st1[2] == 0 and st1[3] == 10       # receiver 8: 16 - 5 - 8 = 3 rows of (1, 1)
+    for sb in ranks:
+        assert np.array_equal(sb.out.cpu().numpy()[2, :plen], pays[1][0])
+    assert not ranks[1].out.cpu().numpy()[3].any()   # a failed instance's row is all zero
 
 
 @pytest.mark.gpu
@@ -212,16 +252,24 @@ def _gloo_gpu_worker(rank, world, port, q):
         pay, t = _payloads(700 + rank, count, plen, sb.device)
         sb.step(t, DistExchange())
         torch.cuda.synchronize()
-        good = bool((sb.status.cpu() == 0).all()) and \
-            np.array_equal(sb.out.cpu().numpy()[:, :plen], pay)
+        allpay = [_payloads(700 + s, count, plen, sb.device)[0] for s in range(world)]
+        out = sb.out.cpu().numpy()
+        good = bool((sb.status.cpu() == 0).all()) and all(
+            np.array_equal(out[s * count:(s + 1) * count, :plen], allpay[s]) for s in range(world))
         # the pipelined schedule over two sub-batches gives the same result
         subs = [ShardedBroadcast(n, 2, plen, rank, world, device=0) for _ in range(2)]
         pays = [_payloads(800 + 10 * i + rank, 2, plen, subs[i].device) for i in range(2)]
-        pipelined_step(subs, [p[1] for p in pays], DistExchange())
+        timer = CommTimer(subs[0].device)
+        timer.timing = True
+        pipelined_step(subs, [p[1] for p in pays], DistExchange(), timer)
         torch.cuda.synchronize()
-        for sub, (pp, _) in zip(subs, pays):
-            good = good and bool((sub.status.cpu() == 0).all()) and \
-                np.array_equal(sub.out.cpu().numpy()[:, :plen], pp)
+        for i, sub in enumerate(subs):
+            o = sub.out.cpu().numpy()
+            for s in range(world):
+                exp = _payloads(800 + 10 * i + s, 2, plen, sub.device)[0]
+                good = good and np.array_equal(o[2 * s:2 * s + 2, :plen], exp)
+            good = good and bool((sub.status.cpu() == 0).all())
+        good = good and len(timer.spans) == 4 and timer.elapsed_ms() > 0
         q.put((rank, "ok" if good else "mismatch %s" % sb.status.cpu().tolist()))
     except Exception as e:  # pragma: no cover
         q.put((rank, repr(e)))
