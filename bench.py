@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: hbbft Reliable-Broadcast data path on MI355X.
 
-One step = the whole RBC data path over one batch of `count` independent
-broadcast instances already resident in HBM:
+Headline (instance mode).  One step = the whole RBC data path over one batch
+of `count` independent broadcast instances already resident in HBM:
   frame (broadcast.rs:174-189) -> RS encode (193) -> Merkle tree (204) ->
   N proofs (212-222) -> validate all N proofs (254/291, merkle.rs:83-103) ->
   decode_from_shards with f random erasures per instance (563-601: decode
@@ -10,11 +10,23 @@ broadcast instances already resident in HBM:
 value = payload bytes of every instance on every rank / max-over-ranks wall
 time of the K timed steps (GB/s, 1e9).  Multi-GPU: instances are sharded
 across ranks with no data-path collective (weak scaling).
+
+Validator-sharded simulation (the `validators` object of the same line, or
+the headline with --mode validators): the N validators are split over the
+ranks, Value is an all-to-all and Echo an all-gather over RCCL (xGMI), every
+rank decodes every instance for the receivers it hosts (hbbft_amd/sharded.py).
+
+`python bench.py --gpus N` without torch.distributed.run launches the N rank
+processes itself (before any GPU call); under torch.distributed.run the
+ranks come from the environment.  Inputs are generated on the device from the
+same counter PRNG as the CPU baseline (oracle/rbc_oracle.c orc_gen_payload /
+orc_gen_present), so both legs see identical payloads and erasure patterns.
 """
 import argparse
-import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,17 +35,18 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_OPS = 78.6e12        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (32-bit lane-ops/s)
-KECCAK_OPS_PER_PERM = 4320     # ~180 VALU ops/round x 24 rounds
+KECCAK_OPS_PER_PERM = 4320     # static count: 180 VALU per round x 24 rounds
 # measured ceiling of the Keccak-f[1600] round code itself (register-only loop,
 # 4 waves/SIMD, profiles/r1_valu_microbench.txt): v_alignbit issues at half rate
 KECCAK_CEILING_PERMS = 10.48e9
+SEED = 0x48424246              # "HBBF"
 
 CONFIGS = {
-    # name: (N, payload bytes, instances per GPU, erasures)
-    "cfg2": (16, 1 << 20, 4096, "f"),
-    "cfg3": (64, 256 << 10, 16384, "f"),
-    "cfg4": (128, 256 << 10, 8192, "f"),
-    "cfg5": (250, 4 << 20, 1024, "worst"),
+    # name: (N, payload bytes, instances per GPU, erasures, validator-mode proposals per GPU)
+    "cfg2": (16, 1 << 20, 4096, "f", 512),
+    "cfg3": (64, 256 << 10, 16384, "f", 4096),
+    "cfg4": (128, 256 << 10, 8192, "f", 2048),
+    "cfg5": (250, 4 << 20, 1024, "worst", 128),
 }
 METRIC = "RBC encode+Merkle+decode payload GB/s, N=64, 1/8 GPUs; fraction of HBM peak"
 
@@ -45,52 +58,234 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--count", type=int, default=0, help="instances per GPU (default: config)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--vcount", type=int, default=0,
+                    help="validator mode: proposals per GPU per step (default: config)")
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="target seconds per CPU rep")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--streams", type=int, default=1,
-                    help="sub-batches per step, each on its own HIP stream (overlap)")
-    ap.add_argument("--own-streams", action="store_true",
-                    help="run each sub-batch on its context's own HIP stream")
-    ap.add_argument("--mode", choices=["instances", "validators"], default=None,
-                    help="instances: every rank runs whole instances, no collective (default "
-                         "except cfg4); validators: simulated validators sharded over the ranks, "
-                         "Value/Echo exchanged by all-to-all (hbbft_amd/sharded.py; default for cfg4)")
+                    help="instance mode: sub-batches per step, each on its own HIP stream")
+    ap.add_argument("--vsubs", type=int, default=4,
+                    help="validator mode with >1 rank: pipelined sub-batches per step")
+    ap.add_argument("--mode", choices=["instances", "validators", "both"], default="both",
+                    help="instances: headline only; validators: the validator-sharded simulation "
+                         "as the headline; both (default): instance headline + a `validators` "
+                         "object measured in the same run")
     return ap.parse_args()
 
 
-def main():
-    args = parse()
+# ----------------------------------------------------------------- launcher --
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn(args):
+    """`--gpus N` outside torch.distributed.run: start N rank processes (this
+    process has touched no GPU) and exit with the worst of their codes."""
+    port = str(free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ---------------------------------------------------------- synthetic inputs --
+GEN_C1 = 0xD6E8FEB86659FD93
+GEN_C2 = 0xA0761D6478BD642F
+M64 = (1 << 64) - 1
+
+
+def _s64(x):
+    x &= M64
+    return x - (1 << 64) if x >> 63 else x
+
+
+def _srl(torch, x, s):
+    """Logical right shift of int64 tensors holding uint64 bit patterns."""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def _mix64(torch, z):
+    """orc_mix64 (SplitMix64 finaliser) on int64 tensors, wrapping like uint64."""
+    z = z + _s64(0x9E3779B97F4A7C15)
+    z = (z ^ _srl(torch, z, 30)) * _s64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(torch, z, 27)) * _s64(0x94D049BB133111EB)
+    return z ^ _srl(torch, z, 31)
+
+
+def gen_payloads(torch, seed, first, count, plen, stride, dev):
+    """orc_gen_payload(seed, first + i, ., plen) for i < count, on the device:
+    [count][stride] uint8, bytes past plen zero."""
+    out = torch.zeros((count, stride), dtype=torch.uint8, device=dev)
+    words = (plen + 7) // 8
+    if words == 0:
+        return out
+    chunk = max(1, (1 << 26) // words)
+    q = torch.arange(words, dtype=torch.int64, device=dev).view(1, -1)
+    for lo in range(0, count, chunk):
+        hi = min(count, lo + chunk)
+        inst = torch.arange(first + lo, first + hi, dtype=torch.int64, device=dev).view(-1, 1)
+        base = _s64(seed * GEN_C1) + inst * _s64(GEN_C2)
+        v = _mix64(torch, base + q)
+        b = v.contiguous().view(torch.uint8).view(hi - lo, words * 8)   # little-endian bytes
+        out[lo:hi, :plen] = b[:, :plen]
+    return out
+
+
+def gen_present(torch, seed, first, count, n, n_erase, dev):
+    """orc_gen_present(seed, first + i, n, n_erase, .): erase the r-th still
+    present index, r = mix64(base + t) mod (n - t), for t < n_erase."""
+    pres = torch.ones((count, n), dtype=torch.uint8, device=dev)
+    inst = torch.arange(first, first + count, dtype=torch.int64, device=dev)
+    base = _s64((seed ^ 0x5EED5EED5EED5EED) * GEN_C1) + inst * _s64(GEN_C2)
+    for t in range(min(n_erase, n)):
+        v = _mix64(torch, base + t)
+        d = n - t
+        hi, lo = _srl(torch, v, 32), v & 0xFFFFFFFF
+        r = ((hi % d) * ((1 << 32) % d) + lo % d) % d        # uint64 v mod d
+        cum = torch.cumsum(pres.to(torch.int64), dim=1) - 1     # rank among present
+        hit = (cum == r.view(-1, 1)) & (pres == 1)
+        pres[hit] = 0
+    return pres
+
+
+# --------------------------------------------------------------- accounting --
+def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase, elapsed,
+                config):
+    """Roofline of the dominant kernel from live per-stage HIP-event times.
+    Sponge kernels are VALU-bound (Keccak-f[1600]); the HBM view is reported
+    beside it."""
+    L = (S + 1 + 135) // 136  # Keccak blocks per leaf (S bytes + pad)
+    # algorithmic bytes per launch (SURVEY 8d per-instance figures x instances per launch)
+    alg = {s_: per_launch * v_ for s_, v_ in {
+        "frame": plen + k * S,
+        # frame folded into the specialised encoder: the encode launch also reads the payload
+        "encode": (k + m) * S + (plen if stages.get("frame", (0.0, 0))[1] == 0 else 0),
+        "leaf_hash": n * (S + 32),
+        "tree_levels": (nc - n) * 96,   # one record = all levels of one tree batch
+        "proofs": n * dslots * 32 * 2 + n,
+        "validate": n * (S + 32 * (dslots + 1) + 1),
+        "decode_matrix": n + m * k,
+        "reconstruct": (k + n_erase) * S,
+        "unframe": k * S + plen,
+    }.items()}
+    perms = {"leaf_hash": per_launch * n * L, "validate": per_launch * (n * L + n * dslots),
+             "tree_levels": per_launch * (n - 1)}
+    live = {s: v for s, v in stages.items() if v[1] > 0}
+    dom = max(live, key=lambda s: live[s][0])
+    dom_ms, dom_launches = live[dom]
+    t = dom_ms / 1e3 / max(dom_launches, 1)
+    hbm_gbs = alg[dom] / t / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            pm = json.load(open(prof)).get("traffic", {})
+            if "%s:%s" % (config, dom) in pm:   # HBM bytes per instance (PMC) x instances
+                traffic = pm["%s:%s" % (config, dom)] * per_launch
+        except (ValueError, OSError):
+            traffic = None
+    step_bytes = sum(alg[s] * (stages[s][1] / max(steps, 1)) for s in stages if s in alg)
+    r = {"kernel": dom, "launch_ms": t * 1e3, "traffic": traffic,
+         "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": hbm_gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg[dom]},
+         "pipeline_alg_bytes_per_step": step_bytes,
+         "pipeline_hbm_frac": step_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS}
+    if dom in perms:
+        opp, src = valu_ops_per_perm()
+        pps = perms[dom] / t
+        ops = pps * opp / 1e12
+        r.update({"bound": "valu", "achieved": ops, "peak": VALU_PEAK_OPS / 1e12,
+                  "unit": "T lane-ops/s", "frac": ops * 1e12 / VALU_PEAK_OPS,
+                  "perms_per_launch": perms[dom], "perms_per_s": pps,
+                  "ops_per_perm": opp, "ops_per_perm_source": src,
+                  "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
+                  "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS})
+    else:
+        r.update({"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": hbm_gbs / HBM_PEAK_GBS})
+    return r
+
+
+def valu_ops_per_perm():
+    """32-bit lane-ops per Keccak-f[1600] of the sponge kernel: SQ_INSTS_VALU x 64
+    / permutations from the committed counter pass, else the static count."""
+    p = os.path.join(ROOT, "profiles", "valu_ops_per_perm.json")
+    try:
+        d = json.load(open(p))
+        return float(d["leaf_hash_kernel"]), "rocprofv3 SQ_INSTS_VALU (%s)" % d["source"]
+    except (OSError, ValueError, KeyError):
+        return float(KECCAK_OPS_PER_PERM), "static: 180 VALU/round x 24"
+
+
+# ------------------------------------------------------------- CPU baseline --
+def cpu_quota():
+    """CPUs of this process's cgroup quota (cgroup v2 cpu.max), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, n, f, plen, n_erase, config):
+    """The same pipeline in oracle/rbc_oracle.c (the reference's algorithm: table
+    GF MACs like pure-Rust galois_8, scalar Keccak like tiny-keccak) on every
+    CPU this process may use and on one, median of --cpu-reps repetitions over
+    the same counter-PRNG payloads and erasure patterns as the GPU leg."""
+    from oracle import pyoracle as orc
+    orc.build()
+    cpus = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
+    threads = max(1, min(cpus, int(quota)) if quota else cpus)
+
+    def measure(th, target_s, cap):
+        t1, _ = orc.bench_pipeline(n, f, plen, th, n_erase, SEED, th)   # calibration
+        per = max(t1, 1e-6)
+        sample = int(max(th, min(cap, target_s / per * th)))
+        times, oks = [], []
+        for _ in range(args.cpu_reps):
+            t, ok = orc.bench_pipeline(n, f, plen, sample, n_erase, SEED, th)
+            times.append(t)
+            oks.append(ok)
+        times.sort()
+        med = times[len(times) // 2]
+        return sample, med, min(oks), times
+
+    sample, med, ok, times = measure(threads, args.cpu_seconds, 4096)
+    s1, med1, ok1, _ = measure(1, args.cpu_seconds / 2, 256)
+    return {"value": sample * plen / med / 1e9, "unit": "GB/s", "cores": threads,
+            "kind": "port", "reps": args.cpu_reps, "host_cpus": os.cpu_count(),
+            "affinity_cpus": cpus, "cgroup_cpu_quota": quota,
+            "single_core": {"value": s1 * plen / med1 / 1e9, "unit": "GB/s", "cores": 1,
+                            "sample": "%d instances, median of %d" % (s1, args.cpu_reps)},
+            "sample": "%d instances of %s (N=%d, %d B payload, %s) through the same pipeline in "
+                      "oracle/rbc_oracle.c on %d threads; median of %d reps %.2f s (min %.2f, "
+                      "max %.2f); %d/%d decoded ok; inputs orc_gen_payload/orc_gen_present("
+                      "seed 0x%X, instance i) = the GPU leg's instances 0..%d"
+                      % (sample, config, n, plen, "f random erasures" if n_erase == f else
+                         "%d random erasures" % n_erase, threads, args.cpu_reps, med, times[0],
+                         times[-1], ok, sample, SEED, sample - 1)}
+
+
+# -------------------------------------------------------------- instance mode --
+def run_instances(args, n, plen, count, erase, rank, world, dev, local):
     import torch
     import torch.distributed as dist
 
     import hbbft_amd as hb
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("HBRBC_BENCH_REHEARSE") == "1":
-        # multi-rank rehearsal on a box with fewer GPUs than ranks: gloo, ranks
-        # share the visible devices (the real N > 1 runs use RCCL, one GPU each)
-        local = local % torch.cuda.device_count()
-        if world > 1:
-            torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
-    elif world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    n, plen, count, erase = CONFIGS[args.config]
-    if args.count:
-        count = args.count
-    mode = args.mode or ("validators" if args.config == "cfg4" else "instances")
-    if mode == "validators":
-        return run_validators(args, n, plen, count, rank, world, local, dev)
     nsub = max(1, min(args.streams, count))
     f = (n - 1) // 3
-    # one Coding context per sub-batch: each owns its reconstruct workspace
     subs_rb = [hb.RbcBatch(n, f, device=local) for _ in range(nsub)]
     rb = subs_rb[0]
     k, m = rb.k, rb.m
@@ -98,18 +293,22 @@ def main():
     stride = rb.stride_for(S)
     n_erase = f if erase == "f" else m
 
-    # ---- inputs resident in HBM before timing ---------------------------
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x48424246 + rank)
+    # ---- inputs resident in HBM before timing (global instance ids) ------
     pstride = (plen + 15) // 16 * 16
-    payloads = torch.randint(0, 256, (count, pstride), dtype=torch.uint8, device=dev, generator=g)
+    first = rank * count
+    payloads = gen_payloads(torch, SEED, first, count, plen, pstride, dev)
     if erase == "f":
-        order = torch.rand((count, n), device=dev, generator=g).argsort(dim=1)
-        present = torch.ones((count, n), dtype=torch.uint8, device=dev)
-        present.scatter_(1, order[:, :n_erase], 0)
+        # fresh random patterns every step (seed SEED + step): a repeating set
+        # would be served by the decode-matrix cache and hide its cost
+        npat = args.warmup + args.steps
+        pool = [gen_present(torch, SEED + s, first, count, n, n_erase, dev) for s in range(npat)]
+        present = pool[0]
     else:  # worst case: only the first k parity shards survive
         present = torch.zeros((count, n), dtype=torch.uint8, device=dev)
         present[:, k:2 * k] = 1
+        for sb in subs_rb:   # one fixed pattern: its specialised decoder (rse's cached matrix)
+            sb.specialise_decoder(present[0].cpu().numpy())
+        pool = [present]
     slab = torch.empty((count, n, stride), dtype=torch.uint8, device=dev)
     nodes = torch.empty((count, rb.node_count, 32), dtype=torch.uint8, device=dev)
     nodes2 = torch.empty_like(nodes)
@@ -123,9 +322,6 @@ def main():
     plen_out = torch.empty(count, dtype=torch.int32, device=dev)
     status = torch.empty(count, dtype=torch.int32, device=dev)
 
-    # sub-batches: contiguous instance ranges, one stream each, so one
-    # sub-batch's VALU-bound hashing overlaps another's HBM-bound copies and
-    # the grid tails of every stage fill (the work per step is unchanged)
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
     main = torch.cuda.current_stream(dev)
     subs = []
@@ -133,310 +329,273 @@ def main():
         lo, hi = bounds[i], bounds[i + 1]
         sb = subs_rb[i]
         sb.reserve(hi - lo)
-        subs.append((sb, (sb.own_stream() if args.own_streams else torch.cuda.Stream(dev))
-                     if nsub > 1 else main, slice(lo, hi)))
+        subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
 
-    def run_sub(sb, sl):
+    def run_sub(sb, sl, pres):
         sb.frame_encode(payloads[sl], plen, slab[sl])   # frame folded into the encoder
         sb.merkle(slab[sl], S, nodes[sl])
         sb.proofs(nodes[sl], digests[sl], ndig[sl])
         sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
         roots[sl].copy_(nodes[sl, -1, :])      # what the Echo/Ready quorum agreed on
-        sb.decode(slab[sl], S, present[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
+        sb.decode(slab[sl], S, pres[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
                   status[sl])
 
-    # Sub-batch streams are joined only where the host synchronises (after the
-    # warm-up and after the timed steps): each stream runs its own sub-batch
-    # step after step, ordered by the stream alone.  After every join the
-    # streams are re-staggered by one stage (stream i starts once stream i-1
-    # has finished its frame+encode), so one sub-batch's HBM-bound stages run
-    # beside another's VALU-bound Keccak instead of in lockstep with it.
-    restagger = [True]
-
-    def step():
+    def step(i):
+        pres = pool[i % len(pool)]
         if nsub == 1:
-            run_sub(subs[0][0], subs[0][2])
+            run_sub(subs[0][0], subs[0][2], pres)
             return
-        first = restagger[0]
-        restagger[0] = False
-        ev = None
-        if first:
-            ev = torch.cuda.Event()
-            ev.record(main)
+        ev = torch.cuda.Event()
+        ev.record(main)
         for sb, st, sl in subs:
-            if first:
-                st.wait_event(ev)
+            st.wait_event(ev)
             with torch.cuda.stream(st):
-                sb.frame_encode(payloads[sl], plen, slab[sl])
-                if first:
-                    ev = torch.cuda.Event()
-                    ev.record(st)
-                sb.merkle(slab[sl], S, nodes[sl])
-                sb.proofs(nodes[sl], digests[sl], ndig[sl])
-                sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
-                roots[sl].copy_(nodes[sl, -1, :])
-                sb.decode(slab[sl], S, present[sl], roots[sl], nodes2[sl], out[sl],
-                          plen_out[sl], status[sl])
+                run_sub(sb, sl, pres)
+        for _, st, _ in subs:
+            main.wait_stream(st)
 
-    def join():
-        torch.cuda.synchronize(dev)
-        restagger[0] = True
-
-    for _ in range(args.warmup):
-        step()
-    join()
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
     if not args.no_verify:
         assert bool((ok == 1).all()), "a valid proof was rejected"
         assert bool((status == 0).all()), "decode failed"
         assert bool((plen_out == plen).all())
         assert torch.equal(out[:, :plen], payloads[:, :plen]), "decoded payload differs"
+        # decode once more from a copy whose erased rows hold garbage: the
+        # timed steps decode in place, where erased rows still hold the right
+        # bytes, so only this pass shows the rebuild itself is correct
+        present = pool[(args.warmup - 1) % len(pool)]
+        vs = slab.clone()
+        vs[present == 0] = 0xA5
+        out.zero_()
+        for sb, _, sl in subs:
+            sb.decode(vs[sl], S, present[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
+                      status[sl])
+        torch.cuda.synchronize(dev)
+        assert bool((status == 0).all()), "decode from garbage-filled erasures failed"
+        assert torch.equal(out[:, :plen], payloads[:, :plen]), "rebuilt payload differs"
+        assert torch.equal(vs, slab) and torch.equal(nodes2, nodes), "rebuilt rows differ"
+        del vs
 
     for sb in subs_rb:
         sb.profile(True)
         sb.profile_reset()
     if world > 1:
         dist.barrier()
-    join()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    join()
-    t1 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
     for sb in subs_rb:
         sb.profile(False)
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev)
     stages = {}
     for sb in subs_rb:
         for st_name, (ms, cnt) in sb.profile_read().items():
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
-
-    total_payload = float(count) * plen * world * args.steps
-    value = total_payload / elapsed / 1e9
-    per_launch = count / nsub          # instances processed by one launch
-
-    # ---- roofline of the dominant kernel (per launch, live HIP events) ---
-    L = (S + 1 + 135) // 136  # Keccak blocks per leaf (S bytes + pad)
-    # algorithmic bytes per launch (SURVEY 8d per-instance figures x instances per launch)
-    alg_bytes = {s_: per_launch * v_ for s_, v_ in {
-        "frame": plen + k * S,
-        # frame folded into the specialised encoder: the encode launch also reads the payload
-        "encode": (k + m) * S + (plen if stages.get("frame", (0.0, 0))[1] == 0 else 0),
-        "leaf_hash": n * (S + 32),
-        "tree_levels": (rb.node_count - n) * 96,   # one record = all levels of one tree batch
-        "proofs": n * rb.dslots * 32 * 2 + n,
-        "validate": n * (S + 32 * (rb.dslots + 1) + 1),
-        "decode_matrix": n + m * k * 16,
-        "reconstruct": (k + n_erase) * S,
-        "unframe": k * S + plen,
-    }.items()}
-    dom = max(stages, key=lambda s: stages[s][0])
-    dom_ms, dom_launches = stages[dom]
-    per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
-    achieved = alg_bytes[dom] / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    perms = {"leaf_hash": per_launch * n * L, "validate": per_launch * (n * L + n * rb.dslots),
-             "tree_levels": per_launch * (n - 1)}
-    valu = None
-    if dom in perms:
-        ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
-        pps = perms[dom] / per_launch_s
-        valu = {"achieved_ops": ops, "peak_ops": VALU_PEAK_OPS, "frac": ops / VALU_PEAK_OPS,
-                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom],
-                "perms_per_s": pps, "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
-                "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS}
-    step_bytes = sum(alg_bytes[s] * (stages[s][1] / max(args.steps, 1)) for s in stages)
-    roofline = {
-        "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "launch_ms": per_launch_s * 1e3,
-        "valu": valu,
-        "pipeline_alg_bytes_per_step": step_bytes,
-        "pipeline_hbm_frac": step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,
+    value = float(count) * plen * world * args.steps / elapsed / 1e9
+    roof = roofline_of(stages, args.steps, count / nsub, n, k, m, S, plen, rb.node_count,
+                       rb.dslots, n_erase, elapsed, args.config)
+    return {
+        "value": value, "ms_per_step": elapsed / args.steps * 1e3, "roofline": roof,
+        "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
+        "config": {"workload": "%s: N=%d f=%d (%d+%d shards), %d B payloads, %d instances/GPU, "
+                               "%s erasures" % (args.config, n, f, k, m, plen, count,
+                                                "f random" if erase == "f" else "worst-case"),
+                   "n": n, "f": f, "payload_bytes": plen, "shard_len": S,
+                   "instances_per_gpu": count, "global_batch": count * world,
+                   "parallelism": "instance-sharded x%d" % world, "streams_per_gpu": nsub},
+        "n_erase": n_erase, "f": f,
     }
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            pm = json.load(open(prof)).get("traffic", {})
-            key = "%s:%s" % (args.config, dom)
-            if key in pm:   # HBM bytes per instance from the PMC pass x instances per launch
-                roofline["traffic"] = pm[key] * per_launch
-        except Exception:
-            pass
-
-    # ---- CPU baseline: the oracle (reference algorithm) on host cores -----
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import pyoracle as orc
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
-        orc.build()
-        cal = max(threads, 2)
-        t_cal, ok_cal = orc.bench_pipeline(n, f, plen, cal, n_erase, 1, threads)
-        sample = int(max(cal, min(4096, args.cpu_seconds / max(t_cal, 1e-6) * cal)))
-        t_cpu, ok_cpu = orc.bench_pipeline(n, f, plen, sample, n_erase, 2, threads)
-        cpu = {"value": sample * plen / t_cpu / 1e9, "unit": "GB/s", "cores": threads,
-               "kind": "port",
-               "sample": "%d instances of %s (N=%d, %d B payload) through the same pipeline in "
-                         "oracle/rbc_oracle.c on %d pthreads, %.1f s, %d/%d decoded ok"
-                         % (sample, args.config, n, plen, threads, t_cpu, ok_cpu, sample)}
-
-    if rank == 0:
-        line = {
-            "metric": METRIC, "value": value, "unit": "GB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (uniform random payloads resident in HBM; random erasures)",
-            "config": {"workload": "%s: N=%d f=%d (%d+%d shards), %d B payloads, %d instances/GPU, "
-                                   "%s erasures" % (args.config, n, f, k, m, plen, count,
-                                                    "f random" if erase == "f" else "worst-case"),
-                       "n": n, "f": f, "payload_bytes": plen, "shard_len": S,
-                       "instances_per_gpu": count, "global_batch": count * world,
-                       "parallelism": "instance-sharded x%d" % world,
-                       "streams_per_gpu": nsub},
-            "roofline": roofline, "cpu_baseline": cpu,
-            "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
-def run_validators(args, n, plen, count, rank, world, local, dev):
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ------------------------------------------------------------ validator mode --
+def run_validators(args, n, plen, count, rank, world, dev, local):
     """Validator-sharded simulation: each rank proposes `count`
-    instances and hosts N/world validators; Value and Echo rows cross ranks
-    in two all-to-alls (RCCL over xGMI), roots in an all-gather."""
+    instances per step and hosts N/world validators; Value rows cross ranks in
+    an all-to-all, Echo rows in an all-gather (RCCL over xGMI), and every rank
+    decodes every instance for its receivers."""
     import torch
     import torch.distributed as dist
 
-    from hbbft_amd.sharded import DistExchange, ShardedBroadcast, SoloExchange, pipelined_step
+    from hbbft_amd.sharded import (CommTimer, DistExchange, ShardedBroadcast, SoloExchange,
+                                   pipelined_step)
 
-    # more than one rank: 4 pipelined sub-batches unless --streams says otherwise
-    nsub = max(1, min(args.streams if args.streams > 1 else 4, count)) if world > 1 else 1
+    nsub = max(1, min(args.vsubs, count)) if world > 1 else 1
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
     subs = [ShardedBroadcast(n, bounds[i + 1] - bounds[i], plen, rank, world, device=local)
             for i in range(nsub)]
     sb = subs[0]
     ex = DistExchange() if world > 1 else SoloExchange()
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x48424246 + rank)
+    timer = CommTimer(dev)
     pstride = (plen + 15) // 16 * 16
-    payloads = torch.randint(0, 256, (count, pstride), dtype=torch.uint8, device=dev, generator=g)
-    pay_sub = [payloads[bounds[i]:bounds[i + 1]] for i in range(nsub)]
-    xev = []   # (start, end) events around the two exchanges, on torch's stream
+    # instance (rank s, local i) is global instance s * count + i
+    pay_sub = [gen_payloads(torch, SEED, rank * count + bounds[i], bounds[i + 1] - bounds[i], plen,
+                            pstride, dev) for i in range(nsub)]
 
-    def step(timed=False):
-        if nsub > 1:   # sub-batches with every exchange in flight behind compute
-            pipelined_step(subs, pay_sub, ex)
-            return
-        sb.propose(payloads)
-        sb.pack_value()
-        a = torch.cuda.Event(enable_timing=True) if timed else None
-        if a:
-            a.record()
-        sb.exchange_value(ex)
-        if a:
-            b = torch.cuda.Event(enable_timing=True)
-            b.record()
-            xev.append((a, b))
-        sb.validate_values()
-        a = torch.cuda.Event(enable_timing=True) if timed else None
-        if a:
-            a.record()
-        sb.exchange_echo(ex)
-        if a:
-            b = torch.cuda.Event(enable_timing=True)
-            b.record()
-            xev.append((a, b))
-        sb.decode()
+    def step():
+        if world > 1:   # sub-batches with every exchange in flight behind compute
+            pipelined_step(subs, pay_sub, ex, timer)
+        else:
+            sb.step(pay_sub[0], ex)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if not args.no_verify:
-        real = len(sb.topo.validators(rank))
         for i, s_ in enumerate(subs):
-            assert bool((s_.ok_v[:, :, :real] == 1).all()), "a valid Value proof was rejected"
+            c = bounds[i + 1] - bounds[i]
+            assert bool((s_.ok_v == 1).all()), "a valid Value proof was rejected"
             assert bool((s_.status == 0).all()), "decode failed"
             assert bool((s_.plen_out == plen).all())
-            assert torch.equal(s_.out[:, :plen], pay_sub[i][:, :plen]), "decoded payload differs"
+            for src in range(world):   # every rank decoded every rank's instances
+                exp = gen_payloads(torch, SEED, src * count + bounds[i], c, plen, pstride, dev)
+                assert torch.equal(s_.out[src * c:(src + 1) * c, :plen], exp[:, :plen]), \
+                    "decoded payload differs"
     for s_ in subs:
         s_.rb.profile(True)
         s_.rb.profile_reset()
+    timer.reset()
+    timer.timing = world > 1
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(timed=True)
+        step()
     torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
     for s_ in subs:
         s_.rb.profile(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
+    elapsed = max_over_ranks(elapsed, world, dev)
+    xms = timer.elapsed_ms() / args.steps if world > 1 else 0.0
+    timer.timing = False
     stages = {}
+    counts = {}
     for s_ in subs:
         for st_name, (ms, cnt) in s_.rb.profile_read().items():
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
-    count_launch = count // nsub
-    xms = sum(a.elapsed_time(b) for a, b in xev)
-    S, k, m = sb.S, sb.rb.k, sb.rb.m
-    L = (S + 1 + 135) // 136
-    alg_bytes = {"frame": plen + k * S, "encode": (k + m) * S, "leaf_hash": n * (S + 32),
-                 "validate": n * (S + 32 * (sb.rb.dslots + 1) + 1), "reconstruct": (k + sb.topo.f) * S,
-                 "unframe": k * S + plen}
-    dom = max(alg_bytes, key=lambda s_: stages[s_][0])
-    dom_ms, dom_launches = stages[dom]
-    per_launch_s = dom_ms / 1e3 / max(dom_launches, 1)
-    achieved = alg_bytes[dom] * count_launch / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    perms = {"leaf_hash": count_launch * n * L,
-             "validate": count_launch * (n * L + n * sb.rb.dslots)}
-    valu = None
-    if dom in perms:
-        ops = perms[dom] * KECCAK_OPS_PER_PERM / per_launch_s
-        pps = perms[dom] / per_launch_s
-        valu = {"achieved_ops": ops, "peak_ops": VALU_PEAK_OPS, "frac": ops / VALU_PEAK_OPS,
-                "ops_per_perm": KECCAK_OPS_PER_PERM, "perms_per_launch": perms[dom],
-                "perms_per_s": pps, "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
-                "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS}
-    xbytes = 2 * (world - 1) / world * count * sb.topo.npad * sb.stride
+        for key, v in s_.counts().items():
+            counts[key] = counts.get(key, 0) + v
+    t = sb.topo
+    # bytes each rank moves per step: Value all-to-all sends (G-1)/G of its
+    # slab + digests; the Echo all-gather brings in the other ranks' rows of
+    # every instance; the roots all-gather is 32 B per instance
+    xbytes = ((world - 1) / world * count * t.npad * (sb.stride + sb.dsz)
+              + (world - 1) * count * t.npad * (sb.stride + sb.dsz)
+              + (world - 1) * count * 32) if world > 1 else 0.0
     value = float(count) * plen * world * args.steps / elapsed / 1e9
+    return {
+        "value": value, "unit": "GB/s", "ms_per_step": elapsed / args.steps * 1e3,
+        "scaling": "weak in proposals (every rank decodes all world x count instances)",
+        "config": {"workload": "%s validator-sharded: N=%d f=%d (%d+%d shards), %d B payloads, %d "
+                               "proposals/GPU/step, validators in blocks of %d over %d GPUs, Value "
+                               "all-to-all + Echo all-gather, every GPU decodes every instance"
+                               % (args.config, n, t.f, sb.rb.k, sb.rb.m, plen, count, t.rpg, world),
+                   "proposals_per_gpu": count, "instances_per_step": count * world,
+                   "parallelism": "validator-sharded x%d" % world,
+                   "pipelined_sub_batches": nsub},
+        "exchange": {"ms_per_step": xms, "bytes_per_step_per_gpu": xbytes,
+                     "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
+                     "backend": getattr(ex, "dist", None) and ex.dist.get_backend()
+                     if world > 1 else "none"},
+        "work_per_step_rank0": counts,
+        "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
+    }
+
+
+# --------------------------------------------------------------------- main --
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn(args)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    rehearse = os.environ.get("HBRBC_BENCH_REHEARSE") == "1"
+    if rehearse:
+        # multi-rank rehearsal on a box with fewer GPUs than ranks: gloo, ranks
+        # share the visible devices (the real N > 1 runs use RCCL, one GPU each)
+        local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus
+        assert rehearse or dist.get_backend() == "nccl", "multi-GPU runs use RCCL"
+
+    n, plen, count, erase, vcount = CONFIGS[args.config]
+    count = args.count or count
+    vcount = args.vcount or vcount
+    head = vobj = None
+    if args.mode in ("instances", "both"):
+        head = run_instances(args, n, plen, count, erase, rank, world, dev, local)
+    if args.mode in ("validators", "both"):
+        torch.cuda.empty_cache()
+        vobj = run_validators(args, n, plen, vcount, rank, world, dev, local)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        f = (n - 1) // 3
+        cpu = cpu_baseline(args, n, f, plen, f if erase == "f" else 2 * f, args.config)
+
     if rank == 0:
-        line = {
-            "metric": METRIC, "value": value, "unit": "GB/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (uniform random payloads resident in HBM)",
-            "config": {"workload": "%s: N=%d f=%d (%d+%d shards), %d B payloads, %d proposals/GPU, "
-                                   "validators sharded over %d GPUs (%d each), Value + Echo "
-                                   "all-to-all, receiver misses its f right-hand Echoes"
-                                   % (args.config, n, sb.topo.f, k, m, plen, count, world,
-                                      sb.topo.rpg),
-                       "n": n, "f": sb.topo.f, "payload_bytes": plen, "shard_len": S,
-                       "instances_per_gpu": count, "global_batch": count * world,
-                       "parallelism": "validator-sharded x%d" % world,
-                       "pipelined_sub_batches": nsub},
-            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "launch_ms": per_launch_s * 1e3, "valu": valu},
-            "exchange": {"ms_per_step": xms / args.steps, "bytes_per_step_per_gpu": xbytes,
-                         "GBps_per_gpu": xbytes / (xms / args.steps / 1e3) / 1e9 if xms else None},
-            "cpu_baseline": None,
-            "stages_ms_per_step": {s_: stages[s_][0] / args.steps for s_ in stages},
-        }
+        if head is not None:
+            line = {
+                "metric": METRIC, "value": head["value"], "unit": "GB/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                "data": "synthetic (counter-PRNG payloads and f-erasure patterns generated in "
+                        "HBM, identical to the CPU baseline's)",
+                "config": head["config"], "roofline": head["roofline"], "cpu_baseline": cpu,
+                "stages_ms_per_step": head["stages_ms_per_step"],
+            }
+            if vobj is not None:
+                if cpu is not None:
+                    vobj["cpu_baseline"] = dict(cpu, note="the same per-instance pipeline; the "
+                                                "CPU leg decodes each instance once")
+                line["validators"] = vobj
+        else:
+            line = {
+                "metric": METRIC, "value": vobj["value"], "unit": "GB/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": vobj["ms_per_step"],
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                "data": "synthetic (counter-PRNG payloads generated in HBM)",
+                "config": vobj["config"], "roofline": None, "cpu_baseline": cpu,
+                "validators": vobj,
+            }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

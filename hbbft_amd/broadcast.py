@@ -256,6 +256,7 @@ class Broadcast:
                 raise
             raise BroadcastError(ErrorKind.InvalidNodeCount)
         self._k, self._m = data, parity
+        self.device = device if device >= 0 else 0   # batched helpers run on this GPU
         self.value_sent = False
         self.echo_sent = False
         self.ready_sent = False
@@ -516,17 +517,17 @@ class Broadcast:
         return "%r Broadcast(%r)" % (self.our_id, self.proposer_id)
 
 
-def prevalidate(messages, n, backend=None):
+def prevalidate(messages, n, backend=None, device=0):
     """Validate the proofs of many pending Value / Echo messages (of any number
-    of Broadcast instances over n validators) in one batched launch before
-    they are delivered.  `Proof::validate` is a pure function of the proof, so
-    the results, memoised on each Proof, are exactly what every receiver's
-    `validate_proof` (broadcast.rs:604-606) would compute; the receiver's
-    index check stays in the state machine."""
+    of Broadcast instances over n validators) in one batched launch on
+    `device` before they are delivered.  `Proof::validate` is a pure function
+    of the proof, so the results, memoised on each Proof, are exactly what
+    every receiver's `validate_proof` (broadcast.rs:604-606) would compute; the
+    receiver's index check stays in the state machine."""
     be = backend if backend is not None else _default_backend()
     fn = getattr(be, "validate_proofs", None)
     if fn is not None:
-        fn([m.payload for m in messages if m.kind <= Message.ECHO], n)
+        fn([m.payload for m in messages if m.kind <= Message.ECHO], n, device=device)
 
 
 def broadcast_many(inputs, backend=None):
@@ -539,11 +540,24 @@ def broadcast_many(inputs, backend=None):
     proofs exactly as `broadcast` does.  Error checks stay per instance and
     come first, as in `broadcast`."""
     be = backend if backend is not None else _default_backend()
+    # all-or-nothing: every input is checked before any instance changes state,
+    # so an error leaves every instance able to propose again
+    seen = set()
+    for bc, _ in inputs:
+        if bc.our_id != bc.proposer_id:
+            raise BroadcastError(ErrorKind.InstanceCannotPropose)
+        if bc.value_sent or id(bc) in seen:
+            raise BroadcastError(ErrorKind.MultipleInputs)
+        seen.add(id(bc))
     fn = getattr(be, "send_shards_batch", None)
-    todo = [(bc, bytes(v)) for bc, v in inputs
-            if bc.our_id == bc.proposer_id and not bc.value_sent]
+    todo = [(bc, bytes(v)) for bc, v in inputs]
     trees = {}
     if fn is not None and todo:
-        for (bc, v), t in zip(todo, fn([(bc.val_set.num(), v) for bc, v in todo])):
-            trees[id(bc)] = t
-    return [bc.broadcast(v, trees.get(id(bc))) for bc, v in inputs]
+        by_dev = {}
+        for bc, v in todo:   # each instance's trees are built on its own GPU
+            by_dev.setdefault(bc.device, []).append((bc, v))
+        for dev, group in by_dev.items():
+            for (bc, v), t in zip(group, fn([(bc.val_set.num(), v) for bc, v in group],
+                                            device=dev)):
+                trees[id(bc)] = t
+    return [bc.broadcast(v, trees.get(id(bc))) for bc, v in todo]

@@ -98,7 +98,7 @@ class Proof:
                 self._digests == other._digests and self._root == other._root)
 
 
-def validate_proofs(proofs, n):
+def validate_proofs(proofs, n, device=0):
     """Checker twin of hbbft_amd.validate_proofs (one 'launch' per call)."""
     todo = {id(p): p for p in proofs if n not in p._valid}
     for p in todo.values():
@@ -138,7 +138,7 @@ class MerkleTree:
 SEND_STATS = {"trees": 0, "launches": 0}
 
 
-def send_shards_batch(items):
+def send_shards_batch(items, device=0):
     """Checker twin of hbbft_amd.send_shards_batch: orc.send_shards per item
     (frame + encode + tree of broadcast.rs:170-204)."""
     out = []

@@ -1,0 +1,40 @@
+"""bench.py's host logic on CPU: the device-side input generators restate the
+oracle's counter PRNG (orc_gen_payload / orc_gen_present), so the GPU leg and
+the CPU baseline see identical payloads and erasure patterns; the launcher
+refuses a rank count that disagrees with --gpus."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import torch
+
+import bench
+from oracle import pyoracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_payload_generator_matches_oracle():
+    for plen, first, count in [(262144, 0, 3), (1000, 17, 4), (7, 5, 2), (0, 0, 2), (4096, 1 << 20, 2)]:
+        out = bench.gen_payloads(torch, bench.SEED, first, count, plen, max(16, plen + 9),
+                                 "cpu").numpy()
+        for i in range(count):
+            assert np.array_equal(out[i, :plen], orc.gen_payload(bench.SEED, first + i, plen))
+            assert not out[i, plen:].any()
+
+
+def test_present_generator_matches_oracle():
+    for n, n_erase, first, count in [(64, 21, 0, 50), (16, 5, 1000, 30), (250, 166, 3, 5),
+                                     (4, 1, 0, 20), (128, 42, 99, 10)]:
+        pres = bench.gen_present(torch, bench.SEED, first, count, n, n_erase, "cpu").numpy()
+        for i in range(count):
+            assert np.array_equal(pres[i], orc.gen_present(bench.SEED, first + i, n, n_erase)), \
+                (n, i)
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

@@ -401,6 +401,29 @@ def test_broadcast_many_errors(backend):
     assert e.value.kind == ErrorKind.MultipleInputs
 
 
+def test_broadcast_many_is_all_or_nothing(backend):
+    """A failing input anywhere in the list (a non-proposer, the same instance
+    twice) raises before any instance changes state, so the valid proposers
+    can still broadcast afterwards (no stalled instances)."""
+    ids = list(range(4))
+    a = Broadcast(0, ids, 0, backend=backend)
+    b = Broadcast(2, ids, 2, backend=backend)
+    other = Broadcast(1, ids, 0, backend=backend)
+    with pytest.raises(BroadcastError) as e:
+        broadcast_many([(a, b"one"), (b, b"two"), (other, b"x")], backend)
+    assert e.value.kind == ErrorKind.InstanceCannotPropose
+    assert not a.value_sent and not b.value_sent
+    with pytest.raises(BroadcastError) as e:
+        broadcast_many([(a, b"one"), (a, b"again")], backend)
+    assert e.value.kind == ErrorKind.MultipleInputs
+    assert not a.value_sent
+    steps = broadcast_many([(a, b"one"), (b, b"two")], backend)
+    assert a.value_sent and b.value_sent and len(steps) == 2
+    fresh = Broadcast(2, ids, 2, backend=backend).broadcast(b"two")
+    assert [(repr(t.target), t.message) for t in steps[1].messages] == \
+        [(repr(t.target), t.message) for t in fresh.messages]
+
+
 @pytest.mark.gpu
 def test_send_shards_batch_matches_oracle():
     """hbbft_amd.send_shards_batch (batched frame+encode+tree on the MI355X)
