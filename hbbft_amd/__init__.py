@@ -108,6 +108,8 @@ def lib():
         "hbrbc_jit_build_encode_group": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p]),
         "hbrbc_jit_file_name": (ctypes.c_int, [_S, _S, _S, ctypes.c_char_p, _S]),
         "hbrbc_frame_encode_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _P, _S, _S, _S, _S, _S, _P]),
+        "hbrbc_frame_encode_ragged": (ctypes.c_int, [_P, _P, _S, _P, _S, _S, _P, _S, _S, _P]),
+        "hbrbc_merkle_ragged": (ctypes.c_int, [_P, _P, _P, _S, _S, _S, _P, _S, _P]),
         "hbrbc_merkle_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _S, _S, _P, _S, _P]),
         "hbrbc_validate_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _S, _S, _P, _P, _P, _P, _S,
                                                _P, _S, _S, _S, _P, _P, _S, _P]),
@@ -583,6 +585,20 @@ class RbcBatch:
                                           _ptr(ndig), _ptr(roots), roots.stride(0), self.n, count,
                                           _ptr(ok), self._stream(stream)))
 
+    # -- ragged batches (hbrbc.h): proposals of different lengths, one launch per stage
+    def frame_encode_ragged(self, payloads, plens, max_plen, slab, stream=None):
+        """payloads [count, >=max_plen]; plens int32 device [count]; slab [count, n, stride]
+        with stride >= round_up(shard_len(max_plen), 16)."""
+        _check(lib().hbrbc_frame_encode_ragged(self.coding.handle, _ptr(payloads),
+                                               payloads.stride(0), _ptr(plens), max_plen,
+                                               slab.shape[0], _ptr(slab), slab.stride(1),
+                                               slab.stride(0), self._stream(stream)))
+
+    def merkle_ragged(self, slab, slens, nodes, stream=None):
+        _check(lib().hbrbc_merkle_ragged(self.coding.handle, _ptr(slab), _ptr(slens),
+                                         slab.stride(1), slab.stride(0), slab.shape[0],
+                                         _ptr(nodes), nodes.stride(0), self._stream(stream)))
+
     # -- blocked row layouts (hbrbc.h "*_rows"): row j of instance i at
     #    base + i*inst_stride + (j // rpb)*block_stride + (j % rpb)*shard_stride
     def frame_encode_rows(self, payloads, plen, base, count, shard_stride, rows_per_block,
@@ -717,10 +733,11 @@ def send_shards_batch(items, device=0):
     `MerkleTree::from_vec`) for many proposals at once, e.g. the N
     contributions of one Subset / HoneyBadger epoch (subset/proposal_state.rs
     :69-113, honey_badger/epoch_state.rs:223-236), or many epochs.
-    items: [(n, value bytes)].  Proposals with the same validator count and
-    payload length share one frame+encode and one tree launch
-    (hbrbc_frame_encode_batch, hbrbc_merkle_batch); returns one `MerkleTree`
-    per item, equal to the per-call from_vec over the encoded shards."""
+    items: [(n, value bytes)].  Proposals with the same validator count share
+    one frame+encode launch and one tree launch whatever their lengths
+    (hbrbc_frame_encode_batch / hbrbc_merkle_batch when the lengths agree,
+    the ragged forms when they do not); returns one `MerkleTree` per item,
+    equal to the per-call from_vec over the encoded shards."""
     import numpy as np
     import torch
     if not torch.cuda.is_available():
@@ -728,28 +745,38 @@ def send_shards_batch(items, device=0):
     out = [None] * len(items)
     groups = {}
     for i, (n, value) in enumerate(items):
-        groups.setdefault((int(n), len(value)), []).append(i)
+        groups.setdefault(int(n), []).append(i)
     dev = torch.device("cuda", device)
-    for (n, plen), idx in groups.items():
+    for n, idx in groups.items():
         rb = _SEND_BATCH.get((n, device))
         if rb is None:
             rb = _SEND_BATCH[(n, device)] = RbcBatch(n, device=device)
-        count, S = len(idx), shard_len(plen, rb.k)
-        pay = np.zeros((count, max(16, (plen + 15) // 16 * 16)), np.uint8)
+        count = len(idx)
+        lens = [len(items[i][1]) for i in idx]
+        pmax = max(lens)
+        Ss = [shard_len(L, rb.k) for L in lens]
+        pay = np.zeros((count, max(16, (pmax + 15) // 16 * 16)), np.uint8)
         for r, i in enumerate(idx):
-            if plen:
-                pay[r, :plen] = np.frombuffer(bytes(items[i][1]), np.uint8)
+            if lens[r]:
+                pay[r, :lens[r]] = np.frombuffer(bytes(items[i][1]), np.uint8)
         payloads = torch.from_numpy(pay).to(dev)
-        slab = rb.alloc_slab(count, S)
         nodes = rb.alloc_nodes(count)
-        if rb.m:
-            rb.frame_encode(payloads, plen, slab)
-        else:   # Coding::Trivial (N <= 3): no parity
-            rb.frame(payloads, plen, slab)
-        rb.merkle(slab, S, nodes)
+        if len(set(lens)) == 1:
+            S = Ss[0]
+            slab = rb.alloc_slab(count, S)
+            if rb.m:
+                rb.frame_encode(payloads, pmax, slab)
+            else:   # Coding::Trivial (N <= 3): no parity
+                rb.frame(payloads, pmax, slab)
+            rb.merkle(slab, S, nodes)
+        else:       # ragged: one launch per stage for every length
+            slab = rb.alloc_slab(count, shard_len(pmax, rb.k))
+            rb.frame_encode_ragged(payloads, torch.tensor(lens, dtype=torch.int32, device=dev),
+                                   pmax, slab)
+            rb.merkle_ragged(slab, torch.tensor(Ss, dtype=torch.int32, device=dev), nodes)
         sl, nd = slab.cpu().numpy(), nodes.cpu().numpy()
         for r, i in enumerate(idx):
-            out[i] = MerkleTree([sl[r, j, :S].tobytes() for j in range(n)], nd[r].copy())
+            out[i] = MerkleTree([sl[r, j, :Ss[r]].tobytes() for j in range(n)], nd[r].copy())
         SEND_STATS["trees"] += count
         SEND_STATS["launches"] += 1
     return out

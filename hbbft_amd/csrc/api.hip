@@ -528,13 +528,20 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v11.co";
+           "_v12.co";
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
 int spec_depth() {
     if (const char *e = getenv("HBRBC_JIT_DEPTH")) return std::max(1, std::min(8, atoi(e)));
     return 4;
+}
+
+// Lockstep interval (input rows between workgroup barriers) of the
+// specialised kernels; 0 = none.  HBRBC_JIT_SYNC overrides (A/B).
+int spec_sync() {
+    if (const char *e = getenv("HBRBC_JIT_SYNC")) return std::max(0, std::min(64, atoi(e)));
+    return 0;
 }
 
 bool read_file(const std::string &path, std::vector<char> &out) {
@@ -571,7 +578,8 @@ int spec_row_tile(size_t nin, size_t nout) {
 XorProgram encode_program(size_t k, size_t m, const uint8_t *parity_rows, int rt, int depth,
                           int r_lo, int r_hi, int rb) {
     XorProgram p;
-    p.name = encode_kernel_name(k, m, rt, depth, r_lo, rb);
+    p.sync = spec_sync();
+    p.name = encode_kernel_name(k, m, rt, depth, r_lo, rb, p.sync);
     for (size_t j = 0; j < k; ++j) p.in_rows.push_back((int)j);
     for (int r = r_lo; r < r_hi; ++r) p.out_rows.push_back((int)(k + r));
     p.coefs.assign(parity_rows + (size_t)r_lo * k, parity_rows + (size_t)r_hi * k);
@@ -595,7 +603,8 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
     out.clear();
     for (size_t gi = 0; gi < groups.size(); ++gi) {
         XorProgram p;
-        p.name = decode_kernel_name(n, hash, rt, depth, (int)gi, rb);
+        p.sync = spec_sync();
+        p.name = decode_kernel_name(n, hash, rt, depth, (int)gi, rb, p.sync);
         p.in_rows = valid;
         p.out_rows.assign(missing.begin() + groups[gi].first, missing.begin() + groups[gi].second);
         p.coefs.assign(rows.begin() + (size_t)groups[gi].first * k,
@@ -687,7 +696,7 @@ hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, X
     hipFunction_t fn = fused ? g.fe : g.fn;
     if (!spec_pass_split()) {
         a.p_only = -1;
-        const unsigned threads = 64u * (unsigned)std::min(4, npass);
+        const unsigned threads = 64u * (unsigned)xor_waves(npass);
         return hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args, nullptr);
     }
     // one launch per pass, one wave per workgroup: every wave on the chip
@@ -1034,6 +1043,61 @@ int hbrbc_frame_encode_batch(hbrbc_ctx *c, const uint8_t *payloads, size_t paylo
                              size_t shard_stride, size_t inst_stride, void *stream) {
     return hbrbc_frame_encode_rows(c, payloads, payload_stride, payload_len, count, shards,
                                    shard_len, shard_stride, 0, 0, inst_stride, stream);
+}
+
+int hbrbc_frame_encode_ragged(hbrbc_ctx *c, const uint8_t *payloads, size_t payload_stride,
+                              const uint32_t *payload_lens, size_t max_payload_len, size_t count,
+                              uint8_t *shards, size_t shard_stride, size_t inst_stride,
+                              void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (count == 0) return HBRBC_OK;
+    if (!payload_lens) return fail(HBRBC_E_INVALID_ARG, "null payload_lens");
+    const size_t smax = hbrbc_shard_len(max_payload_len, c->k);
+    if (shard_stride < round_up(smax, 16))
+        return fail(HBRBC_E_INVALID_ARG, "shard_stride %zu < round_up(%zu, 16)", shard_stride, smax);
+    int st = check_payloads(c, payloads, payload_stride, max_payload_len, smax);
+    if (st) return st;
+    st = check_slab(shards, shard_stride, shard_stride, inst_stride, c->n, count);
+    if (st) return st;
+    HB_HIP(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    const RowMap rows = plain_rows(shard_stride);
+    {
+        StageTimer t(c, HBRBC_STAGE_FRAME, s);
+        HB_HIP(launch_frame(payloads, payload_stride, max_payload_len, count, shards, smax, rows,
+                            inst_stride, c->k, s, payload_lens, shard_stride));
+    }
+    if (c->m == 0) return HBRBC_OK;
+    // rows are zero past each instance's shard: one encode over the common row length
+    return encode_rows(c, shards, shard_stride, rows, inst_stride, count, s);
+}
+
+int hbrbc_merkle_ragged(hbrbc_ctx *c, const uint8_t *shards, const uint32_t *shard_lens,
+                        size_t shard_stride, size_t inst_stride, size_t count, uint8_t *nodes,
+                        size_t node_inst_stride, void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (count == 0) return HBRBC_OK;
+    if (!shard_lens) return fail(HBRBC_E_INVALID_ARG, "null shard_lens");
+    int st = check_slab(shards, shard_stride, shard_stride, inst_stride, c->n, count);
+    if (st) return st;
+    st = check_nodes(nodes, node_inst_stride, c->n, count);
+    if (st) return st;
+    HB_HIP(hipSetDevice(c->device));
+    hipStream_t s = pick(c, stream);
+    {
+        StageTimer t(c, HBRBC_STAGE_LEAF_HASH, s);
+        HB_HIP(launch_leaf_hash(shards, shard_stride, plain_rows(shard_stride), inst_stride, c->n,
+                                count, nodes, node_inst_stride, s, shard_lens));
+    }
+    StageTimer t(c, HBRBC_STAGE_TREE_LEVELS, s);
+    size_t off = 0, sz = c->n;
+    while (sz > 1) {
+        const size_t nsz = (sz + 1) / 2;
+        HB_HIP(launch_tree_level(nodes, node_inst_stride, off, sz, off + sz, nsz, count, s));
+        off += sz;
+        sz = nsz;
+    }
+    return HBRBC_OK;
 }
 
 int hbrbc_merkle_rows(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, size_t shard_stride,
@@ -1655,7 +1719,7 @@ int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t 
                                             groups.size());
     const std::string f =
         jit_file("", encode_kernel_name(data_shards, parity_shards, rt, spec_depth(),
-                                        groups[group].first, rb)).substr(1);
+                                        groups[group].first, rb, spec_sync())).substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
     std::memcpy(buf, f.c_str(), f.size() + 1);
     return HBRBC_OK;

@@ -19,15 +19,15 @@
 // cost occupancy and it measured slower (5.7 -> 9.0 ms, cfg3).
 //
 // Layout and lane mapping are those of gf_bitslice_kernel: a lane owns 32
-// consecutive byte positions of every row; a workgroup holds up to 4 waves
-// over the same positions, wave w producing passes w, w+4, ... of rt output
-// rows.  Rows are addressed through one buffer resource per row block (the
+// consecutive byte positions of every row; a workgroup holds one wave per
+// pass (up to 8) over the same positions, wave w producing passes w, w+8, ...
+// of rt output rows.  Rows are addressed through one buffer resource per row block (the
 // blocked layouts of the validator-sharded simulation, launchers.hpp RowMap)
 // and an SGPR row offset.  Output is bit-identical to the generic kernel
 // (tests compare both with the oracle).
 //
 // Code objects are cached as files under <lib dir>/jit (names from
-// encode_kernel_name / decode_kernel_name + "_v11.co");
+// encode_kernel_name / decode_kernel_name + "_v12.co");
 // __graft_entry__.build() pre-generates the encoders of the BASELINE
 // validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
@@ -229,6 +229,9 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
     const int depth = fused ? std::min(p.depth, 2) : p.depth;  // 36 bytes per row in flight when fused
     const int nbuf = depth + 1;
     const int rb = p.rb;
+    // every wave runs exactly one pass only when npass <= 8 waves: only then
+    // do all waves reach the same barriers
+    const bool lockstep = p.sync > 0 && npass <= 8 && npass > 1;
     const CoefView cv{p.coefs.data(), nin};
     auto blk = [&](int row) { return row / rb; };
     auto rin = [&](int row) { return row % rb; };
@@ -236,7 +239,11 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
     for (int r : p.in_rows) blocks.insert(blk(r));
     for (int r : p.out_rows) blocks.insert(blk(r));
     std::ostringstream o;
-    o << "\nextern \"C\" __global__ __launch_bounds__(256) void " << p.name << (fused ? "_fe" : "")
+    // one wave per pass (up to 8): the waves of a workgroup stream the same
+    // input rows together, so each row comes from HBM about once per program
+    // (4 waves over 6 passes fetched 4.6x the input at cfg5, PMC FETCH_SIZE)
+    o << "\nextern \"C\" __global__ __launch_bounds__(" << xor_waves(npass) * 64 << ") void "
+      << p.name << (fused ? "_fe" : "")
       << "(uint8_t *__restrict__ base, unsigned long inst_stride, unsigned long shard_stride,\n"
          "    unsigned long block_stride, unsigned row_bytes, unsigned waves_per_row,\n"
          "    const uint8_t *__restrict__ payloads, unsigned long payload_stride, unsigned P, unsigned S,\n"
@@ -363,6 +370,11 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
             // over all inputs and keeps every input's planes live at once
             o << "        for (int t_ = 0; t_ < " << rows << "; ++t_) for (int q_ = 0; q_ < 8; ++q_) "
                  "__asm__ volatile(\"\" : \"+v\"(a[t_][q_]));\n      }\n";
+            // lockstep: the passes of a workgroup meet every `sync` rows, so a
+            // row's bytes are fetched once and served from L1/L2 to the other
+            // waves (a plain s_barrier: the prefetched rows stay in flight)
+            if (lockstep && (jj + 1) % (size_t)p.sync == 0 && jj + 1 < nin)
+                o << "      __builtin_amdgcn_s_barrier();\n";
         }
         o << "      if (active) {\n";
         for (int t = 0; t < rows; ++t) {
@@ -382,20 +394,26 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
 
 }  // namespace
 
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb) {
+int xor_waves(int npass) { return std::max(1, std::min(8, npass)); }
+
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb,
+                               int sync) {
     char b[128];
     snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d", k, m, rt, depth, r_lo);
     std::string s = b;
     if (rb < 256) s += "_b" + std::to_string(rb);
+    if (sync > 0) s += "_s" + std::to_string(sync);
     return s;
 }
 
-std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb) {
+std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb,
+                               int sync) {
     char b[128];
     snprintf(b, sizeof b, "hbrbc_dec_n%zu_%016llx_rt%d_d%d_g%d", n, (unsigned long long)hash, rt,
              depth, group);
     std::string s = b;
     if (rb < 256) s += "_b" + std::to_string(rb);
+    if (sync > 0) s += "_s" + std::to_string(sync);
     return s;
 }
 

@@ -25,6 +25,9 @@ struct XorProgram {
     std::vector<int> in_rows, out_rows;
     std::vector<uint8_t> coefs;  // [out_rows.size()][in_rows.size()]
     int rt = 2, depth = 4, rb = 256;
+    // > 0: a raw s_barrier after every `sync` input rows (every wave runs one
+    // pass, so the waves of a workgroup stream the input rows in lockstep)
+    int sync = 0;
     uint64_t guard = 0;
     bool fused = false;
 };
@@ -43,14 +46,18 @@ struct XorArgs {
     int p_only;
 };
 
+// Waves per workgroup of a program with npass passes (one per pass, <= 8).
+int xor_waves(int npass);
 std::string gen_xor_source(const XorProgram &p);
 // hiprtc-compile a generated source for gfx950 (no device needed).  0 on success.
 int compile_source(const std::string &src, std::vector<char> &code, std::string &log);
 
 // Names: encoder group (k, m, rt, depth, first parity row, rows per block)
 // and decoder group (n, pattern hash, rt, depth, group, rows per block).
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb);
-std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb);
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb,
+                               int sync = 0);
+std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb,
+                               int sync = 0);
 // Output-row groups [lo, hi), one hiprtc program each (large matrices are
 // split so each program stays near 4096 coefficients).
 std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt);

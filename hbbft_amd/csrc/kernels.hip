@@ -74,15 +74,23 @@ __device__ __forceinline__ uint4 load16_shifted(const uint8_t *src, uint32_t sh)
 // One thread per 16-byte chunk of every data row; the (instance, row) of a
 // workgroup is scalar.  Logical framed byte b (= BE32(len) ++ payload ++ 0s)
 // lives in row b / S at b % S (broadcast.rs:174-189); [S, round16(S)) is zeroed.
+// Ragged batches (plens != nullptr): instance i frames plens[i] bytes into
+// shards of ceil((plens[i] + 4) / k) bytes, and the whole row slot up to
+// row_fill is written (zeros past the shard), so one encode over the common
+// row length serves every instance.
 __global__ __launch_bounds__(kBlock) void frame_kernel(
     const uint8_t *__restrict__ payloads, size_t payload_stride, uint32_t P,
     uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
-    uint32_t k, uint32_t blocks_per_row) {
+    uint32_t k, uint32_t blocks_per_row, const uint32_t *__restrict__ plens, uint32_t row_fill) {
     const uint32_t grow = blockIdx.x / blocks_per_row;  // instance * k + j
     const uint32_t chunk = (blockIdx.x - grow * blocks_per_row) * kBlock + threadIdx.x;
     const uint32_t off = chunk * 16;
-    if (off >= ((S + 15u) & ~15u)) return;
     const size_t inst = grow / k;
+    if (plens) {   // P = the batch's maximum: a longer entry would read past its row
+        P = min(plens[inst], P);
+        S = (P + 4u + k - 1u) / k;
+    }
+    if (off >= (row_fill ? row_fill : ((S + 15u) & ~15u))) return;
     const uint32_t j = grow - (uint32_t)inst * k;
     uint4 *dst = reinterpret_cast<uint4 *>(shards + inst * inst_stride + rows.off(j) + off);
     if (off >= S) {
@@ -312,13 +320,16 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
 // ----------------------------------------------------------- leaf hashes --
 // One SHA3-256 sponge per lane: lane g hashes shard (g % n) of instance
 // (g / n).  All lanes share the shard length, so every branch is uniform.
+// (slens != nullptr: ragged batch, instance i's shards are slens[i] bytes.)
 __global__ __launch_bounds__(kBlock) void leaf_hash_kernel(
     const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
-    uint32_t n, size_t total, uint8_t *__restrict__ nodes, size_t node_inst_stride) {
+    uint32_t n, size_t total, uint8_t *__restrict__ nodes, size_t node_inst_stride,
+    const uint32_t *__restrict__ slens) {
     const size_t g = blockIdx.x * (size_t)kBlock + threadIdx.x;
     if (g >= total) return;
     const size_t inst = g / n;
     const uint32_t i = (uint32_t)(g - inst * n);
+    if (slens) S = slens[inst];
     uint32_t d[8];
     sha3_256_row(shards + inst * inst_stride + rows.off(i), S, d);
     store_digest(nodes + inst * node_inst_stride + (size_t)i * 32, d);
@@ -840,15 +851,17 @@ hipError_t configure_kernels() {
 
 hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
                         size_t count, uint8_t *shards, size_t shard_len, const RowMap &rows,
-                        size_t inst_stride, size_t data_shards, hipStream_t s) {
-    const size_t chunks = (shard_len + 15) / 16;
+                        size_t inst_stride, size_t data_shards, hipStream_t s,
+                        const uint32_t *plens, size_t row_fill) {
+    const size_t chunks = ((plens ? row_fill : shard_len) + 15) / 16;
     if (count == 0 || chunks == 0) return hipSuccess;
     const size_t bpr = (chunks + kBlock - 1) / kBlock;
     const size_t blocks = bpr * count * data_shards;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(frame_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, payloads,
                        payload_stride, (uint32_t)payload_len, shards, (uint32_t)shard_len, rows,
-                       inst_stride, (uint32_t)data_shards, (uint32_t)bpr);
+                       inst_stride, (uint32_t)data_shards, (uint32_t)bpr, plens,
+                       (uint32_t)(plens ? row_fill : 0));
     return hipGetLastError();
 }
 
@@ -914,12 +927,12 @@ int gf_row_tile(int rows) {
 
 hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                             size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
-                            size_t node_inst_stride, hipStream_t s) {
+                            size_t node_inst_stride, hipStream_t s, const uint32_t *slens) {
     const size_t total = n * count;
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
                        shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len, rows,
-                       inst_stride, (uint32_t)n, total, nodes, node_inst_stride);
+                       inst_stride, (uint32_t)n, total, nodes, node_inst_stride, slens);
     return hipGetLastError();
 }
 

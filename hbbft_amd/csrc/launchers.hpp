@@ -31,9 +31,12 @@ inline RowMap plain_rows(size_t sst) {
 }
 
 // Frame `count` payloads into the data rows of a shard slab (zero padding).
+// plens != nullptr: a ragged batch, instance i frames plens[i] bytes (its own
+// shard length) and fills its row slots up to row_fill bytes.
 hipError_t launch_frame(const uint8_t *payloads, size_t payload_stride, size_t payload_len,
                         size_t count, uint8_t *shards, size_t shard_len, const RowMap &rows,
-                        size_t inst_stride, size_t data_shards, hipStream_t s);
+                        size_t inst_stride, size_t data_shards, hipStream_t s,
+                        const uint32_t *plens = nullptr, size_t row_fill = 0);
 
 // The last payload_len & 3 payload bytes of a fused frame+encode: data byte
 // plus its GF(2^8) contribution to every parity row (matrix = n x k, device).
@@ -77,7 +80,8 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s);
 // SHA3 of every shard row -> level 0 of each instance's node slab.
 hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                             size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
-                            size_t node_inst_stride, hipStream_t s);
+                            size_t node_inst_stride, hipStream_t s,
+                            const uint32_t *slens = nullptr);
 // SHA3 of only the rows a reconstruct rebuilt (out_idx of each instance's
 // decode-matrix slot) -> their level-0 nodes; the other leaves are already
 // there (decode with known leaves).

@@ -154,6 +154,24 @@ int hbrbc_encode_batch(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t
 int hbrbc_frame_encode_batch(hbrbc_ctx *ctx, const uint8_t *payloads, size_t payload_stride,
                              size_t payload_len, size_t count, uint8_t *shards, size_t shard_len,
                              size_t shard_stride, size_t inst_stride, void *stream);
+/* ---- ragged batches: one launch per stage for proposals of any lengths ---- */
+/* send_shards' framing + Coding::encode (broadcast.rs:174-193) for `count`
+ * proposals of their own lengths, e.g. an epoch where every validator
+ * proposes its contribution (honey_badger/epoch_state.rs:223-236,
+ * subset/proposal_state.rs:69-113): instance i frames payload_lens[i]
+ * (device uint32[count], each <= max_payload_len) bytes into shards of
+ * ceil((payload_lens[i] + 4) / data) bytes; every row slot is written up to
+ * shard_stride (>= round_up(shard_len(max_payload_len), 16)), zero past the
+ * instance's shard, and the parity rows are encoded over that common length. */
+int hbrbc_frame_encode_ragged(hbrbc_ctx *ctx, const uint8_t *payloads, size_t payload_stride,
+                              const uint32_t *payload_lens, size_t max_payload_len, size_t count,
+                              uint8_t *shards, size_t shard_stride, size_t inst_stride,
+                              void *stream);
+/* MerkleTree::from_vec of a ragged batch: leaf j of instance i hashes
+ * shard_lens[i] (device uint32[count]) bytes of its row. */
+int hbrbc_merkle_ragged(hbrbc_ctx *ctx, const uint8_t *shards, const uint32_t *shard_lens,
+                        size_t shard_stride, size_t inst_stride, size_t count, uint8_t *nodes,
+                        size_t node_inst_stride, void *stream);
 /* MerkleTree::from_vec over the n = data+parity shards of every instance
  * (broadcast.rs:204, 580). */
 int hbrbc_merkle_batch(hbrbc_ctx *ctx, const uint8_t *shards, size_t shard_len,

@@ -427,13 +427,17 @@ def test_broadcast_many_is_all_or_nothing(backend):
 @pytest.mark.gpu
 def test_send_shards_batch_matches_oracle():
     """hbbft_amd.send_shards_batch (batched frame+encode+tree on the MI355X)
-    against the oracle's send_shards for ragged payloads at N = 1..64: every
-    shard, every tree node and every proof bit-exact."""
+    against the oracle's send_shards for ragged payloads at N = 1..64 -- each
+    N one ragged launch per stage: every shard, every tree node and every
+    proof bit-exact."""
     hb = _hip_backend()
     orb = _oracle_backend()
     items = [(n, bytes((13 * n + 5 * i + j) & 0xFF for j in range(L)))
              for n in (1, 2, 3, 4, 7, 16, 64) for i, L in enumerate((0, 1, 5, 5, 100, 1000, 4099, 1000))]
+    before = dict(hb.SEND_STATS)
     got = hb.send_shards_batch(items)
+    # one frame+encode and one tree launch per validator count, whatever the lengths (f3)
+    assert hb.SEND_STATS["launches"] - before["launches"] == 7
     want = orb.send_shards_batch(items)
     for (n, _), g, w in zip(items, got, want):
         assert g.values() == w.values()
