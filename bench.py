@@ -463,6 +463,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
             c = bounds[i + 1] - bounds[i]
             assert bool((s_.ok_v == 1).all()), "a valid Value proof was rejected"
             assert bool((s_.status == 0).all()), "decode failed"
+            assert bool(s_.decided.all()), "an instance missed its Ready quorum / CanDecode"
             assert bool((s_.plen_out == plen).all())
             for src in range(world):   # every rank decoded every rank's instances
                 exp = gen_payloads(torch, SEED, src * count + bounds[i], c, plen, pstride, dev)

@@ -47,8 +47,12 @@ class RseError(Exception):
 
     def __init__(self, code, msg=""):
         self.code = code
+        self.msg = msg
         self.name = STATUS_NAMES.get(code, "Status%d" % code)
         super().__init__("%s%s" % (self.name, (": " + msg) if msg else ""))
+
+    def __reduce__(self):   # picklable across process pools (build() workers)
+        return (RseError, (self.code, self.msg))
 
 
 _lib = None

@@ -528,13 +528,20 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v12.co";
+           "_v14.co";
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
 int spec_depth() {
     if (const char *e = getenv("HBRBC_JIT_DEPTH")) return std::max(1, std::min(8, atoi(e)));
     return 4;
+}
+
+// Payload rows in flight of the frame+encode twins (36 loaded bytes per row
+// and lane).  HBRBC_JIT_FDEPTH overrides (A/B).
+int spec_fdepth() {
+    if (const char *e = getenv("HBRBC_JIT_FDEPTH")) return std::max(1, std::min(8, atoi(e)));
+    return 2;
 }
 
 // Lockstep interval (input rows between workgroup barriers) of the
@@ -568,10 +575,13 @@ bool write_file(const std::string &path, const std::vector<char> &code) {
 // per row) plus the planes, pair XORs and load buffers must stay near 200
 // VGPRs (2 waves/SIMD) without spilling.
 int spec_row_tile(size_t nin, size_t nout) {
-    if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(16, atoi(e) & ~1));
-    // split matrices: 8-row passes keep each program's straight-line passes
-    // (and so its compile time) small
-    return nin * nout > 4096 ? 8 : gf_row_tile((int)nout);
+    // (passes are balanced: rt is the longest pass; HBRBC_RT_SPEC overrides, A/B)
+    if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(24, atoi(e)));
+    // split matrices (N = 250): 12-row passes of the pairwise network, four
+    // per 48-row program (cfg5 encode 14.7 -> 12.4 ms, worst-case
+    // reconstruct 13.1 -> 11.4 ms against 8-row nibble passes; 16 rows:
+    // 17.4 / 16.6 ms)
+    return nin * nout > 4096 ? 12 : gf_row_tile((int)nout);
 }
 
 // The encoder program of parity-row group [r_lo, r_hi) for row block rb.
@@ -579,7 +589,8 @@ XorProgram encode_program(size_t k, size_t m, const uint8_t *parity_rows, int rt
                           int r_lo, int r_hi, int rb) {
     XorProgram p;
     p.sync = spec_sync();
-    p.name = encode_kernel_name(k, m, rt, depth, r_lo, rb, p.sync);
+    p.fdepth = spec_fdepth();
+    p.name = encode_kernel_name(k, m, rt, depth, r_lo, r_hi, rb, p.sync, p.fdepth);
     for (size_t j = 0; j < k; ++j) p.in_rows.push_back((int)j);
     for (int r = r_lo; r < r_hi; ++r) p.out_rows.push_back((int)(k + r));
     p.coefs.assign(parity_rows + (size_t)r_lo * k, parity_rows + (size_t)r_hi * k);
@@ -604,7 +615,8 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
     for (size_t gi = 0; gi < groups.size(); ++gi) {
         XorProgram p;
         p.sync = spec_sync();
-        p.name = decode_kernel_name(n, hash, rt, depth, (int)gi, rb, p.sync);
+        p.name = decode_kernel_name(n, hash, rt, depth, groups[gi].first, groups[gi].second, rb,
+                                    p.sync);
         p.in_rows = valid;
         p.out_rows.assign(missing.begin() + groups[gi].first, missing.begin() + groups[gi].second);
         p.coefs.assign(rows.begin() + (size_t)groups[gi].first * k,
@@ -1006,7 +1018,8 @@ int hbrbc_frame_encode_rows(hbrbc_ctx *c, const uint8_t *payloads, size_t payloa
     if (c->m > 0 && shard_stride == round_up(shard_len, 16) && payload_len <= 0x7FFFFFFFull &&
         shard_len * c->k < 0x7FFFFFFFull)
         gs = spec_encoder(c, code_rb(rows));
-    if (!gs) {
+    const char *fe = getenv("HBRBC_FUSE");   // 0: frame kernel + encoder (A/B)
+    if (!gs || (fe && !std::strcmp(fe, "0"))) {
         st = frame_rows(c, payloads, payload_stride, payload_len, count, shards, shard_len, rows,
                         inst_stride, s);
         if (st || c->m == 0) return st;
@@ -1719,7 +1732,8 @@ int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t 
                                             groups.size());
     const std::string f =
         jit_file("", encode_kernel_name(data_shards, parity_shards, rt, spec_depth(),
-                                        groups[group].first, rb, spec_sync())).substr(1);
+                                        groups[group].first, groups[group].second, rb,
+                                        spec_sync(), spec_fdepth())).substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
     std::memcpy(buf, f.c_str(), f.size() + 1);
     return HBRBC_OK;

@@ -27,7 +27,7 @@
 // (tests compare both with the oracle).
 //
 // Code objects are cached as files under <lib dir>/jit (names from
-// encode_kernel_name / decode_kernel_name + "_v12.co");
+// encode_kernel_name / decode_kernel_name + "_v14.co");
 // __graft_entry__.build() pre-generates the encoders of the BASELINE
 // validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
@@ -80,13 +80,20 @@ __device__ __forceinline__ void hb_window(const u32x4 q0, const u32x4 q1, const 
 // before logical byte 4).  pay = the instance's payload row.
 __device__ __forceinline__ void hb_frame_slow(const uint8_t *pay, unsigned P, unsigned lb,
                                               uint32_t (&x)[8]) {
-    for (int i = 0; i < 8; ++i) x[i] = 0u;
-    for (unsigned i = 0; i < 32u; ++i) {
-        const unsigned b = lb + i;
-        // payload bytes past P & ~3 are left 0 here as in the fast path: the
-        // host's frame_fixup kernel adds them (and their parity) afterwards
-        const unsigned v = b < 4u ? (P >> (8u * (3u - b))) & 0xFFu : (b - 4u < (P & ~3u) ? pay[b - 4u] : 0u);
-        x[i >> 2] |= v << (8u * (i & 3u));
+    // the byte loop stays rolled: unrolled, its 32 per-byte bounds tests were
+    // hoisted out of the pass loop as 64 SGPRs per row (265 SGPR spills in
+    // the fused encoder)
+    _Pragma("unroll") for (int d = 0; d < 8; ++d) {
+        uint32_t w = 0u;
+#pragma nounroll
+        for (unsigned i = 0; i < 4u; ++i) {
+            const unsigned b = lb + 4u * (unsigned)d + i;
+            // payload bytes past P & ~3 are left 0 here as in the fast path: the
+            // host's frame_fixup kernel adds them (and their parity) afterwards
+            const unsigned v = b < 4u ? (P >> (8u * (3u - b))) & 0xFFu : (b - 4u < (P & ~3u) ? pay[b - 4u] : 0u);
+            w |= v << (8u * i);
+        }
+        x[d] = w;
     }
 }
 // 8x32 bit transpose of 8 dwords (three delta swaps; an involution)
@@ -120,8 +127,8 @@ struct CoefView {
 // by this input are built once (<= 11 + 11 ops) and shared by every row of
 // the pass; each accumulator then takes exactly one op.  Fewer VALU than the
 // pairwise network but more values live across the row, so it is used for
-// short passes only (rt <= 8, the split N = 250 programs: encode 16.9 ->
-// 15.0 ms per 1024 instances; at rt 14 it costs 2 waves/SIMD of occupancy).
+// short passes only (rt <= 8; at rt 14 it cost 2 waves/SIMD of occupancy,
+// and the N = 250 programs run faster with 12-row pairwise passes).
 void gen_nibble_network(std::ostringstream &o, const CoefView &cv, int t0, int rows, size_t jj) {
     std::vector<std::pair<int, int>> tgt((size_t)rows * 8, {0, 0});
     bool used[2][16] = {};
@@ -224,9 +231,12 @@ void gen_pair_network(std::ostringstream &o, const CoefView &cv, int t0, int row
 std::string gen_xor_kernel(const XorProgram &p, bool fused) {
     const size_t nin = p.in_rows.size();
     const int nout = (int)p.out_rows.size();
-    const int rt = p.rt;
-    const int npass = (nout + rt - 1) / rt;
-    const int depth = fused ? std::min(p.depth, 2) : p.depth;  // 36 bytes per row in flight when fused
+    // npass passes of at most rt rows, balanced (42 rows at rt 12: 11, 11,
+    // 10, 10 rather than 12, 12, 12, 6 -- the longest pass sets the time)
+    const int npass = (nout + p.rt - 1) / p.rt;
+    auto pass_lo = [&](int ps) { return ps * (nout / npass) + std::min(ps, nout % npass); };
+    const int rt = (nout + npass - 1) / npass;
+    const int depth = fused ? p.fdepth : p.depth;  // 36 bytes per row in flight when fused
     const int nbuf = depth + 1;
     const int rb = p.rb;
     // every wave runs exactly one pass only when npass <= 8 waves: only then
@@ -304,14 +314,19 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
          "  const int p_st = p_only >= 0 ? 1 : nw;\n"
          "  for (int p = p_lo; p < p_hi; p += p_st) {\n    switch (p) {\n";
     for (int ps = 0; ps < npass; ++ps) {
-        const int t0 = ps * rt;
-        const int rows = std::min(rt, nout - t0);
+        const int t0 = pass_lo(ps);
+        const int rows = pass_lo(ps + 1) - t0;
         // a distinct barrier opens every case, so no common prefix (the first
         // rows' loads) is hoisted above the switch and kept live across it
         o << "    case " << ps << ": {\n      __asm__ volatile(\"; pass " << ps
           << "\" ::: \"memory\");\n      uint32_t a[" << rows << "][8] = {};\n";
         if (fused)
-            o << "      u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "];\n";
+            // S through an opaque SGPR copy per pass: otherwise every pass's row
+            // offsets (j * S - 4 and its byte shift) are loop-invariant, get
+            // hoisted above the pass loop and spill (41 SGPRs in the cfg3 encoder)
+            o << "      unsigned S_; __asm__ volatile(\"s_mov_b32 %0, %1\" : \"=s\"(S_) : \"s\"(S));\n"
+                 "      const unsigned S = S_;\n"
+                 "      u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "];\n";
         else
             o << "      u32x4 l[" << nbuf << "], h[" << nbuf << "];\n";
         auto load = [&](size_t jj) {
@@ -396,21 +411,22 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
 
 int xor_waves(int npass) { return std::max(1, std::min(8, npass)); }
 
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb,
-                               int sync) {
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int r_hi, int rb,
+                               int sync, int fdepth) {
     char b[128];
-    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d", k, m, rt, depth, r_lo);
+    snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d_%d", k, m, rt, depth, r_lo, r_hi);
     std::string s = b;
     if (rb < 256) s += "_b" + std::to_string(rb);
     if (sync > 0) s += "_s" + std::to_string(sync);
+    if (fdepth != 2) s += "_f" + std::to_string(fdepth);
     return s;
 }
 
-std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb,
-                               int sync) {
+std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int r_lo, int r_hi,
+                               int rb, int sync) {
     char b[128];
-    snprintf(b, sizeof b, "hbrbc_dec_n%zu_%016llx_rt%d_d%d_g%d", n, (unsigned long long)hash, rt,
-             depth, group);
+    snprintf(b, sizeof b, "hbrbc_dec_n%zu_%016llx_rt%d_d%d_r%d_%d", n, (unsigned long long)hash,
+             rt, depth, r_lo, r_hi);
     std::string s = b;
     if (rb < 256) s += "_b" + std::to_string(rb);
     if (sync > 0) s += "_s" + std::to_string(sync);
@@ -419,7 +435,9 @@ std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int g
 
 std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt) {
     // a group = one hiprtc program; bigger ones compile superlinearly slowly
-    const size_t kMaxCoefs = 4096;
+    // (HBRBC_JIT_GROUP: coefficients per program, A/B)
+    const char *ge = getenv("HBRBC_JIT_GROUP");
+    const size_t kMaxCoefs = ge ? std::max<size_t>(256, (size_t)atol(ge)) : (size_t)4096;
     std::vector<std::pair<int, int>> g;
     size_t per = nout;
     if (nin * nout > kMaxCoefs) per = std::max<size_t>((size_t)rt, kMaxCoefs / nin / rt * rt);

@@ -28,6 +28,8 @@ struct XorProgram {
     // > 0: a raw s_barrier after every `sync` input rows (every wave runs one
     // pass, so the waves of a workgroup stream the input rows in lockstep)
     int sync = 0;
+    // prefetch depth of the frame+encode twin (its rows are 36 loaded bytes)
+    int fdepth = 2;
     uint64_t guard = 0;
     bool fused = false;
 };
@@ -52,12 +54,13 @@ std::string gen_xor_source(const XorProgram &p);
 // hiprtc-compile a generated source for gfx950 (no device needed).  0 on success.
 int compile_source(const std::string &src, std::vector<char> &code, std::string &log);
 
-// Names: encoder group (k, m, rt, depth, first parity row, rows per block)
-// and decoder group (n, pattern hash, rt, depth, group, rows per block).
-std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int rb,
-                               int sync = 0);
-std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int group, int rb,
-                               int sync = 0);
+// Names: encoder group (k, m, rt, depth, parity rows [r_lo, r_hi), rows per
+// block) and decoder group (n, pattern hash, rt, depth, output rows [r_lo,
+// r_hi) of the pattern's missing-row list, rows per block).
+std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int r_hi, int rb,
+                               int sync = 0, int fdepth = 2);
+std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int r_lo, int r_hi,
+                               int rb, int sync = 0);
 // Output-row groups [lo, hi), one hiprtc program each (large matrices are
 // split so each program stays near 4096 coefficients).
 std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt);

@@ -227,6 +227,10 @@ class ShardedBroadcast:
         idx = torch.arange(rank * R, rank * R + self.vreal, dtype=torch.int32, device=dev)
         self.recv_idx = idx.view(1, self.vreal).expand(G * C, self.vreal).contiguous()
         self.ok_v = torch.zeros((G * C, self.vreal), **u8)
+        # every validator's Value outcome (= whether it sends Echo/EchoHash),
+        # all-gathered with the Echoes: the Ready quorum counts them all
+        self.ok_pad = torch.zeros((G * C, R), **u8)
+        self.okv_all = self.ok_pad.view(1, G * C, R) if G == 1 else torch.zeros((G, G * C, R), **u8)
         self.v_digests = torch.zeros((G * C, R, ds, 32), **u8)
         self.v_ndig = torch.zeros((G * C, R), **u8)
         # Echo all-gather: every row of every instance, [G_v][G*C][R][stride]
@@ -247,6 +251,10 @@ class ShardedBroadcast:
         self.out = torch.zeros((G * C, max(16, (rb.k * S + 15) // 16 * 16)), **u8)
         self.plen_out = torch.zeros(G * C, dtype=torch.int32, device=dev)
         self.status = torch.zeros(G * C, dtype=torch.int32, device=dev)
+        # RBC thresholds per instance (GPU-resident counters)
+        self.echo_senders = torch.zeros(G * C, dtype=torch.int32, device=dev)
+        self.full_echos = torch.zeros(G * C, dtype=torch.int32, device=dev)
+        self.decided = torch.zeros(G * C, dtype=torch.bool, device=dev)
         self.own_cols = torch.tensor([j - rank * R for j in own] or [0], dtype=torch.int64,
                                      device=dev)
         self.own_rows = torch.tensor(own or [0], dtype=torch.int64, device=dev)
@@ -316,13 +324,15 @@ class ShardedBroadcast:
                                 dig, nd, drows, self.roots_all.view(G * C, 32), self.ok_v,
                                 rows=self.vrows_t, indices=self.recv_idx,
                                 leaf_out=self.dec_nodes[:, self.rank * R:])
+        self.ok_pad[:, : self.vreal].copy_(self.ok_v)
 
     # 4. Echo messages: all-gather of the validated rows ------------------------
     def exchange_echo(self, ex, async_op=False):
         if self.world == 1:
             return []
         return [ex.all_gather(self.echo_sh, self.recv_sh, async_op),
-                ex.all_gather(self.echo_dg, self.recv_dg, async_op)]
+                ex.all_gather(self.echo_dg, self.recv_dg, async_op),
+                ex.all_gather(self.okv_all, self.ok_pad, async_op)]
 
     def validate_echoes(self):
         """Proof::validate of every Echo the receiver gets from other ranks'
@@ -352,6 +362,23 @@ class ShardedBroadcast:
         self.rb.decode_rows(self.echo_sh, self.S, self.world * self.count, st, rpb, bst, ist,
                             self.present, self.roots_all.view(-1, 32), self.dec_nodes, self.out,
                             self.plen_out, self.status, known_leaves=True)
+        self.thresholds()
+
+    def thresholds(self):
+        """The state machine's counters for receiver r0, per instance, on the
+        device.  A validator whose Value validated sends Echo to its left nodes
+        and EchoHash to its right ones, and count_echos counts both
+        (broadcast.rs:413-425, 456-468), so Ready goes out once N-f validators
+        validated their Values (310-312, and on f+1 Readys everyone follows,
+        396-402); compute_output then needs > 2f Readys and >= k full Echoes at
+        r0 (526-532).  decided[i]: the receivers output instance i (status
+        tells with what); otherwise no node decides it."""
+        t, G, C = self.topo, self.world, self.count
+        valid = self.okv_all.transpose(0, 1).reshape(G * C, t.npad)[:, : t.n]
+        torch.sum(valid, dim=1, dtype=torch.int32, out=self.echo_senders)
+        torch.sum(self.present, dim=1, dtype=torch.int32, out=self.full_echos)
+        readys = torch.where(self.echo_senders >= t.n - t.f, t.n, 0)
+        torch.logical_and(readys > 2 * t.f, self.full_echos >= self.rb.k, out=self.decided)
 
     def step(self, payloads, ex):
         self.propose(payloads)

@@ -150,6 +150,7 @@ def run_loopback(n, world, count, plen, tamper=None, specialise=True):
             for v, src in enumerate(ranks):
                 dst.echo_sh[v].copy_(src.recv_sh.view(dst.echo_sh[v].shape))
                 dst.echo_dg[v].copy_(src.recv_dg.view(dst.echo_dg[v].shape))
+                dst.okv_all[v].copy_(src.ok_pad)
     for sb in ranks:
         sb.validate_echoes()
         sb.decode()
@@ -181,6 +182,9 @@ def test_sharded_loopback_vs_oracle(n, world, count, plen):
         assert (sb.present.cpu().numpy().sum(axis=1) == n - t.f).all()
         assert (sb.status.cpu().numpy() == 0).all()
         assert (sb.plen_out.cpu().numpy() == plen).all()
+        assert sb.decided.cpu().all()                    # Ready quorum and CanDecode met
+        assert (sb.echo_senders.cpu().numpy() == n).all()
+        assert (sb.full_echos.cpu().numpy() == n - t.f).all()
         out = sb.out.cpu().numpy()
         dn = sb.dec_nodes.cpu().numpy()
         for s in range(world):
@@ -229,6 +233,12 @@ def test_sharded_faulty_rows():
     for sb in ranks:
         assert np.array_equal(sb.out.cpu().numpy()[2, :plen], pays[1][0])
     assert not ranks[1].out.cpu().numpy()[3].any()   # a failed instance's row is all zero
+    # the state machine's thresholds: instance (1, 1) has 8 < N - f = 11 Echo
+    # senders, so no Ready quorum forms and no node decides it, although
+    # receiver 0 could rebuild it; instance (1, 0) keeps 15 senders
+    for sb in ranks:
+        assert sb.echo_senders.cpu().tolist() == [16, 16, 15, 8]
+        assert sb.decided.cpu().tolist() == [True, True, True, False]
 
 
 @pytest.mark.gpu
