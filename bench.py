@@ -294,7 +294,7 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
     n_erase = f if erase == "f" else m
 
     # ---- inputs resident in HBM before timing (global instance ids) ------
-    pstride = (plen + 15) // 16 * 16
+    pstride = (plen + 15) // 16 * 16 + int(os.environ.get("HBRBC_BENCH_PPAD", "0"))
     first = rank * count
     payloads = gen_payloads(torch, SEED, first, count, plen, pstride, dev)
     if erase == "f":
@@ -444,7 +444,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
     sb = subs[0]
     ex = DistExchange() if world > 1 else SoloExchange()
     timer = CommTimer(dev)
-    pstride = (plen + 15) // 16 * 16
+    pstride = (plen + 15) // 16 * 16 + int(os.environ.get("HBRBC_BENCH_PPAD", "0"))
     # instance (rank s, local i) is global instance s * count + i
     pay_sub = [gen_payloads(torch, SEED, rank * count + bounds[i], bounds[i + 1] - bounds[i], plen,
                             pstride, dev) for i in range(nsub)]

@@ -528,7 +528,7 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v14.co";
+           "_v16.co";
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
@@ -542,6 +542,22 @@ int spec_depth() {
 int spec_fdepth() {
     if (const char *e = getenv("HBRBC_JIT_FDEPTH")) return std::max(1, std::min(8, atoi(e)));
     return 2;
+}
+
+// Data-row stores of the frame+encode twins spread over the passes
+// (HBRBC_JIT_SPREAD=0: all in pass 0, A/B).
+bool spec_spread() {
+    const char *e = getenv("HBRBC_JIT_SPREAD");
+    return !(e && !std::strcmp(e, "0"));
+}
+
+// Lane byte positions of the specialised kernels as two 16-byte pieces 1 KB
+// apart: every load and store instruction covers 1 KB of consecutive bytes
+// (cfg3 frame+encode 4.82 -> 4.36 ms against 32 consecutive bytes per lane;
+// HBRBC_JIT_SPLIT=0 builds those, A/B).
+bool spec_split() {
+    const char *e = getenv("HBRBC_JIT_SPLIT");
+    return !(e && !std::strcmp(e, "0"));
 }
 
 // Lockstep interval (input rows between workgroup barriers) of the
@@ -590,7 +606,9 @@ XorProgram encode_program(size_t k, size_t m, const uint8_t *parity_rows, int rt
     XorProgram p;
     p.sync = spec_sync();
     p.fdepth = spec_fdepth();
-    p.name = encode_kernel_name(k, m, rt, depth, r_lo, r_hi, rb, p.sync, p.fdepth);
+    p.spread = spec_spread();
+    p.split = spec_split();
+    p.name = encode_kernel_name(k, m, rt, depth, r_lo, r_hi, rb, p.sync, p.fdepth, p.spread, p.split);
     for (size_t j = 0; j < k; ++j) p.in_rows.push_back((int)j);
     for (int r = r_lo; r < r_hi; ++r) p.out_rows.push_back((int)(k + r));
     p.coefs.assign(parity_rows + (size_t)r_lo * k, parity_rows + (size_t)r_hi * k);
@@ -615,8 +633,9 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
     for (size_t gi = 0; gi < groups.size(); ++gi) {
         XorProgram p;
         p.sync = spec_sync();
+        p.split = spec_split();
         p.name = decode_kernel_name(n, hash, rt, depth, groups[gi].first, groups[gi].second, rb,
-                                    p.sync);
+                                    p.sync, p.split);
         p.in_rows = valid;
         p.out_rows.assign(missing.begin() + groups[gi].first, missing.begin() + groups[gi].second);
         p.coefs.assign(rows.begin() + (size_t)groups[gi].first * k,
@@ -1733,7 +1752,8 @@ int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t 
     const std::string f =
         jit_file("", encode_kernel_name(data_shards, parity_shards, rt, spec_depth(),
                                         groups[group].first, groups[group].second, rb,
-                                        spec_sync(), spec_fdepth())).substr(1);
+                                        spec_sync(), spec_fdepth(), spec_spread(),
+                                        spec_split())).substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
     std::memcpy(buf, f.c_str(), f.size() + 1);
     return HBRBC_OK;

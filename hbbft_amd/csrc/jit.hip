@@ -27,7 +27,7 @@
 // (tests compare both with the oracle).
 //
 // Code objects are cached as files under <lib dir>/jit (names from
-// encode_kernel_name / decode_kernel_name + "_v14.co");
+// encode_kernel_name / decode_kernel_name + "_v16.co");
 // __graft_entry__.build() pre-generates the encoders of the BASELINE
 // validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
@@ -75,26 +75,26 @@ __device__ __forceinline__ void hb_window(const u32x4 q0, const u32x4 q1, const 
     const uint32_t w[9] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3], q2};
     _Pragma("unroll") for (int i = 0; i < 8; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs);
 }
-// Framed bytes [lb, lb + 32) built byte by byte: the rare windows that touch
-// the 4-byte BE32 length prefix (only lanes at offset 0 of rows starting
-// before logical byte 4).  pay = the instance's payload row.
-__device__ __forceinline__ void hb_frame_slow(const uint8_t *pay, unsigned P, unsigned lb,
-                                              uint32_t (&x)[8]) {
-    // the byte loop stays rolled: unrolled, its 32 per-byte bounds tests were
-    // hoisted out of the pass loop as 64 SGPRs per row (265 SGPR spills in
-    // the fused encoder)
-    _Pragma("unroll") for (int d = 0; d < 8; ++d) {
-        uint32_t w = 0u;
-#pragma nounroll
-        for (unsigned i = 0; i < 4u; ++i) {
-            const unsigned b = lb + 4u * (unsigned)d + i;
-            // payload bytes past P & ~3 are left 0 here as in the fast path: the
-            // host's frame_fixup kernel adds them (and their parity) afterwards
-            const unsigned v = b < 4u ? (P >> (8u * (3u - b))) & 0xFFu : (b - 4u < (P & ~3u) ? pay[b - 4u] : 0u);
-            w |= v << (8u * i);
-        }
-        x[d] = w;
-    }
+// split lanes: two 16-byte windows from 20 loaded bytes each (q, q2)
+__device__ __forceinline__ void hb_window2(const u32x4 qa, const uint32_t qa2, const u32x4 qb,
+                                           const uint32_t qb2, unsigned bs, uint32_t (&o)[8]) {
+    const uint32_t w[10] = {qa[0], qa[1], qa[2], qa[3], qa2, qb[0], qb[1], qb[2], qb[3], qb2};
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], bs);
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) o[4 + i] = __builtin_amdgcn_alignbyte(w[i + 6], w[i + 5], bs);
+}
+// The window of a lane whose 32 framed bytes start at lb < 4, i.e. inside
+// the 4-byte BE32 length prefix (broadcast.rs:175-177; only offset 0 of rows
+// with j * S < 4): header bytes hdr[lb..3], then payload bytes 0..
+// q0, q1 = payload dwords 0..7 (HB_LDF clamps that lane's load address to 0).
+__device__ __forceinline__ void hb_frame_head(const u32x4 q0, const u32x4 q1, unsigned P,
+                                              unsigned lb, uint32_t (&x)[8]) {
+    const uint32_t w[9] = {__builtin_bswap32(P), q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], lb);
+}
+// split lanes: only the first 16-byte window starts in the prefix
+__device__ __forceinline__ void hb_frame_head2(const u32x4 qa, unsigned P, unsigned lb, uint32_t (&x)[8]) {
+    const uint32_t w[5] = {__builtin_bswap32(P), qa[0], qa[1], qa[2], qa[3]};
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], lb);
 }
 // 8x32 bit transpose of 8 dwords (three delta swaps; an involution)
 __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
@@ -268,13 +268,18 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
              "    if (sl_ >= hash_slots || slot_hash[sl_] != "
           << g << ") return; }\n";
     }
+    // a lane's 32 byte positions: off..off+15 and off2..off2+15.  Default:
+    // 32 consecutive bytes (off2 = off + 16); split: two 16-byte pieces 1 KB
+    // apart, so every load and store instruction of a wave covers 1 KB of
+    // consecutive bytes instead of 64 pieces of 16 with 16-byte gaps
+    const char *d2 = p.split ? "1024u" : "16u";
     o << "  const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);\n"
-         "  const unsigned chunk = (blockIdx.x - (unsigned)inst * waves_per_row) * 64u + (threadIdx.x & 63u);\n"
-         "  unsigned off = chunk * 32u;\n"
-         "  const bool active = off < row_bytes;\n"
+         "  const unsigned wchunk = blockIdx.x - (unsigned)inst * waves_per_row, lane = threadIdx.x & 63u;\n"
+      << (p.split ? "  unsigned off = wchunk * 2048u + lane * 16u;\n" : "  unsigned off = (wchunk * 64u + lane) * 32u;\n")
+      << "  const bool active = off < row_bytes;\n"
          "  if (!active) off = row_bytes - 16u;\n"
-         "  const bool full = off + 32u <= row_bytes;\n"
-         "  const unsigned off2 = full ? off + 16u : off;\n"
+         "  const bool full = off + " << d2 << " + 16u <= row_bytes;\n"
+         "  const unsigned off2 = full ? off + " << d2 << " : off;\n"
          // raw buffer ops: each row block's base lives in a scalar resource,
          // the row offset (row % rb) * shard_stride in an SGPR (soffset) and
          // the lane offset in one VGPR -- no per-lane 64-bit address per row
@@ -294,7 +299,7 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
         // partial last dword are added, with their parity, by frame_fixup.
         o << "  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(\n"
              "      (void *)(payloads + inst * payload_stride), (short)0, (int)(P & ~3u), 0x00020000);\n"
-             "  const bool edge = !__all(off + 32u <= S);\n"
+             "  const bool edge = !__all(off + " << d2 << " + 16u <= S);\n"
              // dword-aligned start: the 32 framed bytes of a lane are bytes
              // bs..bs+31 of 36 loaded bytes, bs = (j*S - 4) & 3 (uniform per row)
              // (the address add is volatile asm: LLVM would otherwise hoist every
@@ -302,9 +307,22 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
              "#define HB_LDF(Q0, Q1, Q2, j) { unsigned a_; "
              "__asm__ volatile(\"v_add_u32 %0, %1, %2\" : \"=v\"(a_) : \"s\"((j) * S - 4u), \"v\"(off)); "
              "a_ &= ~3u; "
+             // a window starting inside the length prefix loads payload dwords 0..8
+             "if ((j) < 4u && (j) * S + off < 4u) a_ = 0u; "
              "Q0 = __builtin_amdgcn_raw_buffer_load_b128(pr, a_, 0, 0); "
              "Q1 = __builtin_amdgcn_raw_buffer_load_b128(pr, a_ + 16u, 0, 0); "
-             "Q2 = __builtin_amdgcn_raw_buffer_load_b32(pr, a_ + 32u, 0, 0); }\n";
+             "Q2 = __builtin_amdgcn_raw_buffer_load_b32(pr, a_ + 32u, 0, 0); }\n"
+             // split lanes: 20 bytes at each of the two pieces
+             "#define HB_LDF2(QA, QA2, QB, QB2, j) { unsigned a_, b_; "
+             "__asm__ volatile(\"v_add_u32 %0, %1, %2\" : \"=v\"(a_) : \"s\"((j) * S - 4u), \"v\"(off)); "
+             "__asm__ volatile(\"v_add_u32 %0, %1, %2\" : \"=v\"(b_) : \"s\"((j) * S - 4u), \"v\"(off2)); "
+             "a_ &= ~3u; b_ &= ~3u; "
+             "if ((j) < 4u && (j) * S + off < 4u) a_ = 0u; "
+             "QA = __builtin_amdgcn_raw_buffer_load_b128(pr, a_, 0, 0); "
+             "QA2 = __builtin_amdgcn_raw_buffer_load_b32(pr, a_ + 16u, 0, 0); "
+             "QB = __builtin_amdgcn_raw_buffer_load_b128(pr, b_, 0, 0); "
+             "QB2 = __builtin_amdgcn_raw_buffer_load_b32(pr, b_ + 16u, 0, 0); }\n";
+
     // p_only >= 0: this launch runs that one pass with one wave per workgroup
     // (the host launches the passes one after another, so every wave on a CU
     // runs the same straight-line code); p_only < 0: wave w runs passes w,
@@ -326,13 +344,17 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
             // hoisted above the pass loop and spill (41 SGPRs in the cfg3 encoder)
             o << "      unsigned S_; __asm__ volatile(\"s_mov_b32 %0, %1\" : \"=s\"(S_) : \"s\"(S));\n"
                  "      const unsigned S = S_;\n"
-                 "      u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "];\n";
+                 "      u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "]"
+              << (p.split ? ", q3[" + std::to_string(nbuf) + "]" : std::string()) << ";\n";
         else
             o << "      u32x4 l[" << nbuf << "], h[" << nbuf << "];\n";
         auto load = [&](size_t jj) {
             const int b = (int)(jj % nbuf);
             const int row = p.in_rows[jj];
-            if (fused)
+            if (fused && p.split)
+                o << "      HB_LDF2(q0[" << b << "], q2[" << b << "], q1[" << b << "], q3[" << b << "], " << row
+                  << "u)";
+            else if (fused)
                 o << "      HB_LDF(q0[" << b << "], q1[" << b << "], q2[" << b << "], " << row << "u)";
             else
                 o << "      HB_LD(l[" << b << "], h[" << b << "], " << blk(row) << ", " << rin(row) << "u)";
@@ -349,21 +371,30 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
             if (jj + depth < nin) load(jj + depth);
             if (fused) {
                 const std::string c = std::to_string(cur);
-                o << "      { uint32_t x[8];\n"
-                  << "        hb_window(q0[" << c << "], q1[" << c << "], q2[" << c << "], (" << row
-                  << "u * S - 4u) & 3u, x);\n";
+                o << "      { uint32_t x[8];\n";
+                if (p.split)
+                    o << "        hb_window2(q0[" << c << "], q2[" << c << "], q1[" << c << "], q3[" << c
+                      << "], (" << row << "u * S - 4u) & 3u, x);\n";
+                else
+                    o << "        hb_window(q0[" << c << "], q1[" << c << "], q2[" << c << "], (" << row
+                      << "u * S - 4u) & 3u, x);\n";
                 // windows touching the BE32 payload length (broadcast.rs:175-177);
                 // j * S < 4 needs j < 4 since S >= 1
                 if (row < 4)
-                    o << "        if (" << row << "u * S < 4u) { if (off == 0u) hb_frame_slow(payloads + inst * "
-                     "payload_stride, P, " << row << "u * S, x); }\n";
+                    o << "        if (" << row << "u * S < 4u) { if (off == 0u) "
+                      << (p.split ? "hb_frame_head2(q0[" + c + "], " : "hb_frame_head(q0[" + c + "], q1[" + c + "], ")
+                      << "P, " << row << "u * S, x); }\n";
                 // positions >= S of this row belong to the next shard: zero
                 o << "        if (edge) {\n"
                      "          _Pragma(\"unroll\") for (int i_ = 0; i_ < 8; ++i_) {\n"
-                     "            const int lim_ = (int)S - (int)off - 4 * i_;\n"
+                     "            const int lim_ = (int)S - (int)(i_ < 4 ? off + 4 * i_ : off2 + 4 * (i_ - 4));\n"
                      "            x[i_] = lim_ >= 4 ? x[i_] : (lim_ <= 0 ? 0u : x[i_] & (0xFFFFFFFFu >> (8 * (4 - lim_))));\n"
                      "          }\n        }\n";
-                if (ps == 0 && p.out_rows.front() == (int)nin)  // pass 0 of group 0 also writes the framed data row
+                // group 0 also writes the framed data rows, pass jj % npass row jj
+                // (spread over the waves: a store ahead of a load holds that
+                // load's vmcnt wait, and pass 0 storing all 22 rows at cfg3 made
+                // it the workgroup's slowest wave)
+                if (p.out_rows.front() == (int)nin && (p.spread ? (int)(jj % npass) == ps : ps == 0))
                     o << "        if (active) {\n"
                          "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[0], x[1], x[2], x[3]}, rs"
                       << blk(row) << ", off, " << rin(row) << "u * sst, HB_ST_AUX);\n"
@@ -403,7 +434,7 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
         }
         o << "      }\n      break; }\n";
     }
-    o << "    }\n  }\n}\n#undef HB_LD\n" << (fused ? "#undef HB_LDF\n" : "");
+    o << "    }\n  }\n}\n#undef HB_LD\n" << (fused ? "#undef HB_LDF\n#undef HB_LDF2\n" : "");
     return o.str();
 }
 
@@ -412,24 +443,27 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
 int xor_waves(int npass) { return std::max(1, std::min(8, npass)); }
 
 std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int r_hi, int rb,
-                               int sync, int fdepth) {
+                               int sync, int fdepth, bool spread, bool split) {
     char b[128];
     snprintf(b, sizeof b, "hbrbc_enc_k%zu_m%zu_rt%d_d%d_r%d_%d", k, m, rt, depth, r_lo, r_hi);
     std::string s = b;
     if (rb < 256) s += "_b" + std::to_string(rb);
     if (sync > 0) s += "_s" + std::to_string(sync);
     if (fdepth != 2) s += "_f" + std::to_string(fdepth);
+    if (!spread) s += "_w0";
+    if (!split) s += "_c";
     return s;
 }
 
 std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int r_lo, int r_hi,
-                               int rb, int sync) {
+                               int rb, int sync, bool split) {
     char b[128];
     snprintf(b, sizeof b, "hbrbc_dec_n%zu_%016llx_rt%d_d%d_r%d_%d", n, (unsigned long long)hash,
              rt, depth, r_lo, r_hi);
     std::string s = b;
     if (rb < 256) s += "_b" + std::to_string(rb);
     if (sync > 0) s += "_s" + std::to_string(sync);
+    if (!split) s += "_c";
     return s;
 }
 

@@ -30,6 +30,10 @@ struct XorProgram {
     int sync = 0;
     // prefetch depth of the frame+encode twin (its rows are 36 loaded bytes)
     int fdepth = 2;
+    // frame+encode twin: the data-row stores spread over the passes (else pass 0)
+    bool spread = true;
+    // lane byte positions: two 16-byte pieces 1 KB apart (else 32 consecutive)
+    bool split = true;
     uint64_t guard = 0;
     bool fused = false;
 };
@@ -58,9 +62,10 @@ int compile_source(const std::string &src, std::vector<char> &code, std::string 
 // block) and decoder group (n, pattern hash, rt, depth, output rows [r_lo,
 // r_hi) of the pattern's missing-row list, rows per block).
 std::string encode_kernel_name(size_t k, size_t m, int rt, int depth, int r_lo, int r_hi, int rb,
-                               int sync = 0, int fdepth = 2);
+                               int sync = 0, int fdepth = 2, bool spread = true,
+                               bool split = false);
 std::string decode_kernel_name(size_t n, uint64_t hash, int rt, int depth, int r_lo, int r_hi,
-                               int rb, int sync = 0);
+                               int rb, int sync = 0, bool split = true);
 // Output-row groups [lo, hi), one hiprtc program each (large matrices are
 // split so each program stays near 4096 coefficients).
 std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt);

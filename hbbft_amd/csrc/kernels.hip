@@ -8,6 +8,9 @@
 //   Proof::validate    broadcast.rs:604-606, merkle.rs:83-103
 //   RS reconstruct     broadcast.rs:569 -> Coding::reconstruct_shards 682-693
 //   decode tail        broadcast.rs:580-600 (re-tree, root compare, unframe)
+#include <cstdlib>
+#include <cstring>
+
 #include "device_common.hpp"
 #include "launchers.hpp"
 
@@ -223,17 +226,21 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
     const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
     const int *__restrict__ nout_arr, int nout_uniform, const int *__restrict__ pat,
     const uint64_t *__restrict__ slot_hash, uint64_t skip_hash, int hash_slots, int nin,
-    uint32_t waves_per_row) {
+    uint32_t waves_per_row, uint32_t piece) {
     const size_t inst = blockIdx.x / waves_per_row;
     const int slot = pat ? pat[inst] : (int)inst;
     // instances of a pattern with a specialised decoder are left to it
     if (skip_hash && slot < hash_slots && slot_hash[slot] == skip_hash) return;
     const int wave = (int)(threadIdx.x >> 6), nwaves = (int)(blockDim.x >> 6);
-    const uint32_t chunk = (blockIdx.x - (uint32_t)inst * waves_per_row) * 64 + (threadIdx.x & 63);
-    uint32_t off = chunk * 32;
+    // a lane's 32 positions: off..off+15 and off+piece..+15.  piece = 1024:
+    // every load/store instruction of the wave covers 1 KB of consecutive
+    // bytes (16: 64 pieces of 16 B with 16-B gaps, two instructions per line)
+    const uint32_t wchunk = blockIdx.x - (uint32_t)inst * waves_per_row, lane = threadIdx.x & 63;
+    uint32_t off = piece == 16 ? (wchunk * 64 + lane) * 32 : wchunk * 2048 + lane * 16;
     const bool active = off < row_bytes;
     if (!active) off = row_bytes - 16;              // clamped, loads stay in the row
-    const bool full = off + 32 <= row_bytes;        // else only 16 bytes belong to this row
+    const bool full = off + piece + 16 <= row_bytes;  // else only 16 bytes belong to this row
+    const uint32_t d2 = full ? piece : 0;
     uint8_t *ib = base + inst * inst_stride;
     const int nout = nout_arr ? nout_arr[slot] : nout_uniform;
     const int npass = (nout + RT - 1) / RT;
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
         auto load_in = [&](int jj, uint4 &l, uint4 &h) {
             const uint8_t *src = ib + rows.off(iidx[jj < nin ? jj : nin - 1]) + off;
             l = *reinterpret_cast<const uint4 *>(src);
-            h = *reinterpret_cast<const uint4 *>(src + (full ? 16 : 0));
+            h = *reinterpret_cast<const uint4 *>(src + d2);
         };
         auto consume = [&](int jj, const uint4 &lo, const uint4 &h) {
             const uint4 hi = full ? h : make_uint4(0, 0, 0, 0);
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
                     bs_transpose(acc[t]);
                     uint8_t *dst = ib + rows.off(oidx[p * RT + t]) + off;
                     store16_stream(dst, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
-                    if (full) store16_stream(dst + 16, acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
+                    if (full) store16_stream(dst + d2, acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
                 }
             }
         }
@@ -886,11 +893,14 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const int max_rows = a.nout ? a.max_rows : a.nout_uniform;
     const int nw = std::max(1, std::min(4, (max_rows + a.rt - 1) / a.rt));  // waves per block
+    const char *pe = getenv("HBRBC_GF_SPLIT");   // 0: 32 consecutive bytes per lane (A/B)
+    const uint32_t piece = (pe && !strcmp(pe, "0")) ? 16u : 1024u;
 #define HB_BS_LAUNCH(RT, MODE)                                                                   \
     hipLaunchKernelGGL((gf_bitslice_kernel<RT, MODE>), dim3((unsigned)blocks), dim3(64 * nw), 0, \
                        s, a.base, a.inst_stride, a.rows, row_bytes, a.coefs, a.coef_slot_stride, \
                        a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,          \
-                       a.nout_uniform, a.pat, a.slot_hash, a.skip_hash, a.hash_slots, a.nin, wpr)
+                       a.nout_uniform, a.pat, a.slot_hash, a.skip_hash, a.hash_slots, a.nin, wpr,   \
+                       piece)
 #define HB_BS_CASE(RT)                                                                           \
     case RT:                                                                                     \
         if (a.mode == 2)                                                                         \
