@@ -784,3 +784,65 @@ def send_shards_batch(items, device=0):
         SEND_STATS["trees"] += count
         SEND_STATS["launches"] += 1
     return out
+
+
+# --------------------------------------------------------------------------
+# Deferred decodes of many Broadcast instances
+# --------------------------------------------------------------------------
+DECODE_STATS = {"decodes": 0, "launches": 0}
+_DECODE_BATCH = {}
+
+
+def decode_shards_batch(requests, device=0):
+    """`Broadcast::decode_from_shards` (broadcast.rs:563-601) for many
+    instances at once: requests [(n, leaf_values, root)] with leaf_values a
+    list of n shards (bytes, or None when missing) -> [payload bytes or None].
+    Shards of one instance must share one non-zero length, else rse's
+    reconstruct fails (IncorrectShardSize / EmptyShard) and so does the decode;
+    the rest go through hbrbc_decode_batch, one launch per (n, shard length):
+    reconstruct, re-tree over all n shards, root compare, BE32 length,
+    truncating take -- None for every rse error, root mismatch or missing
+    length, as in the reference."""
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        raise HbrbcUnavailable("no GPU visible: the RBC path has no CPU fallback")
+    out = [None] * len(requests)
+    groups = {}
+    for i, (n, leaves, root) in enumerate(requests):
+        lens = {len(v) for v in leaves if v is not None}
+        if len(leaves) != n or len(lens) != 1 or 0 in lens:
+            continue   # TooFewShardsPresent (nothing present) / IncorrectShardSize / EmptyShard
+        groups.setdefault((int(n), lens.pop()), []).append(i)
+    dev = torch.device("cuda", device)
+    for (n, S), idx in groups.items():
+        rb = _DECODE_BATCH.get((n, device))
+        if rb is None:
+            rb = _DECODE_BATCH[(n, device)] = RbcBatch(n, device=device)
+        cnt, stride = len(idx), RbcBatch.stride_for(S)
+        slab = np.zeros((cnt, n, stride), np.uint8)
+        present = np.zeros((cnt, n), np.uint8)
+        roots = np.zeros((cnt, 32), np.uint8)
+        for r, i in enumerate(idx):
+            _, leaves, root = requests[i]
+            for j, v in enumerate(leaves):
+                if v is not None:
+                    slab[r, j, :S] = np.frombuffer(bytes(v), np.uint8)
+                    present[r, j] = 1
+            roots[r] = np.frombuffer(bytes(root), np.uint8)
+        t_slab = torch.from_numpy(slab).to(dev)
+        t_pres = torch.from_numpy(present).to(dev)
+        t_roots = torch.from_numpy(roots).to(dev)
+        nodes = rb.alloc_nodes(cnt)
+        prow = max(16, (rb.k * S + 15) // 16 * 16)
+        pay = torch.empty((cnt, prow), dtype=torch.uint8, device=dev)
+        plen = torch.zeros(cnt, dtype=torch.int32, device=dev)
+        status = torch.zeros(cnt, dtype=torch.int32, device=dev)
+        rb.decode(t_slab, S, t_pres, t_roots, nodes, pay, plen, status)
+        st, pl, py = status.cpu().numpy(), plen.cpu().numpy(), pay.cpu().numpy()
+        for r, i in enumerate(idx):
+            if st[r] == 0:
+                out[i] = py[r, :pl[r]].tobytes()
+        DECODE_STATS["decodes"] += cnt
+        DECODE_STATS["launches"] += 1
+    return out

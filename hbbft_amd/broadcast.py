@@ -267,6 +267,10 @@ class Broadcast:
         self.echos = {}         # sender -> Proof | _EchoHash
         self.can_decodes = {}   # digest -> set(sender)
         self.readys = {}        # sender -> digest
+        # deferred decoding (run_lockstep): a list the decode requests go to
+        # instead of decoding at once; resolve_decodes() completes them
+        self.decode_sink = None
+        self._decode_pending = None
 
     # -- ConsensusProtocol (broadcast.rs:60-88) ------------------------------
     def handle_input(self, value):
@@ -469,10 +473,19 @@ class Broadcast:
         if (self.decided or self._count_readys(h) <= 2 * self.val_set.num_faulty()
                 or self._count_echos_full(h) < self._k):
             return Step()
+        if self._decode_pending is not None:
+            # a second attempt within the same message: same inputs, same outcome
+            # (nothing on success, another decoding fault on failure)
+            self._decode_pending["repeat"] += 1
+            return Step()
         leaf_values = []
         for i in self.val_set.all_ids():
             p = _echo_proof(self.echos[i]) if i in self.echos else None
             leaf_values.append(p.value() if p is not None and p.root_hash() == h else None)
+        if self.decode_sink is not None:
+            self._decode_pending = {"bc": self, "leaf_values": leaf_values, "root": h, "repeat": 0}
+            self.decode_sink.append(self._decode_pending)
+            return Step()
         value = self._decode_from_shards(leaf_values, h)
         if value is not None:
             self.decided = True
@@ -515,6 +528,48 @@ class Broadcast:
 
     def __repr__(self):
         return "%r Broadcast(%r)" % (self.our_id, self.proposer_id)
+
+
+def resolve_decodes(requests, backend=None):
+    """Complete the decodes that Broadcast instances with a `decode_sink`
+    deferred: every `decode_from_shards` (broadcast.rs:563-601)
+    of the batch in one reconstruct + re-tree + root check + unframe launch per
+    (validator count, shard length) through the backend's
+    `decode_shards_batch`, or one call each without it.  Returns [(Broadcast,
+    Step)]: the output (and `decided`) on success, the decoding fault(s) on
+    failure -- what `compute_output` would have returned.  Exact as long as
+    an instance handles no message between its request and this call (one
+    crank per network per round)."""
+    be = backend if backend is not None else _default_backend()
+    if not requests:
+        return []
+    fn = getattr(be, "decode_shards_batch", None)
+    if fn is not None:
+        by_dev = {}
+        for r in requests:
+            by_dev.setdefault(r["bc"].device, []).append(r)
+        values = {}
+        for dev, rs in by_dev.items():
+            out = fn([(r["bc"].val_set.num(), r["leaf_values"], r["root"]) for r in rs], device=dev)
+            for r, v in zip(rs, out):
+                values[id(r)] = v
+    else:
+        values = {id(r): r["bc"]._decode_from_shards(list(r["leaf_values"]), r["root"])
+                  for r in requests}
+    res = []
+    for r in requests:
+        bc, v = r["bc"], values[id(r)]
+        bc._decode_pending = None
+        if v is not None:
+            bc.decided = True
+            s = Step()
+            s.output.append(v)
+        else:
+            s = Step()
+            for _ in range(1 + r["repeat"]):
+                s.fault_log.append(Fault(bc.proposer_id, FaultKind.BroadcastDecoding))
+        res.append((bc, s))
+    return res
 
 
 def prevalidate(messages, n, backend=None, device=0):

@@ -115,12 +115,14 @@ __device__ __forceinline__ void keccak_f1600(uint32_t (&L)[25], uint32_t (&H)[25
     }
 }
 
-#ifndef HB_SPONGE_V16
-#define HB_SPONGE_V16 1
-#endif
 // SHA3-256 of `len` bytes at `p` (8-byte aligned; the 8-byte word holding
 // the last byte must be readable).  Per-lane pointer and length; when every
 // lane of a wave has the same length all branches are wave-uniform.
+// V16: the 16-byte-load variant for grids of few sponges (below).  It is a
+// separate instantiation: compiled into the same kernel as the 8-byte path
+// its two block buffers set the kernel's VGPR count (152 -> 3 waves/SIMD for
+// every grid, 130 without it).
+template <bool V16 = false>
 __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint32_t len,
                                              uint32_t (&out)[8]) {
     uint32_t L[25], H[25];
@@ -128,7 +130,6 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     for (int i = 0; i < 25; ++i) L[i] = H[i] = 0u;
     const uint2 *q = reinterpret_cast<const uint2 *>(p);
     const uint32_t nfull = len / 136u;
-#if HB_SPONGE_V16
     // 16-byte-aligned rows (every slab row): block t starts 8*t mod 16 bytes
     // past a 16-byte boundary, so an even block is eight 16-byte loads and
     // one 8-byte load and an odd block one 8-byte load and eight 16-byte
@@ -137,8 +138,7 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     // the grid holds fewer than 4 waves per SIMD (2^18 lanes): there it hides
     // memory latency (cfg2, 65536 rows: leaf hash 23.6 -> 22.8 ms); at full
     // occupancy (cfg3, 1 M rows) it measured 1 % slower than 8-byte loads.
-    const bool low_occ = (uint64_t)gridDim.x * blockDim.x < (1u << 18);
-    if (nfull >= 2 && low_occ && (reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+    if (V16 && nfull >= 2 && (reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
         uint4 e[8], o[8];
         uint2 e8, o0;
         auto load_even = [&](const uint2 *b) {
@@ -194,7 +194,6 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
             q += 17;
         }
     } else
-#endif
     // Full blocks, software-pipelined: block t+1 is loaded while block t is
     // permuted, so the sponge never waits on memory between permutations
     // (+34 VGPRs; the sponge kernels run at 4 waves/SIMD either way).

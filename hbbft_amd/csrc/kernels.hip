@@ -328,7 +328,11 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
 // One SHA3-256 sponge per lane: lane g hashes shard (g % n) of instance
 // (g / n).  All lanes share the shard length, so every branch is uniform.
 // (slens != nullptr: ragged batch, instance i's shards are slens[i] bytes.)
-__global__ __launch_bounds__(kBlock) void leaf_hash_kernel(
+// Sponge kernels: at most 128 VGPRs (4 waves/SIMD, the residency the
+// Keccak ceiling was measured at); V16 = few-sponge grids (16-byte loads).
+#define HB_SPONGE_ATTR __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(V16 ? 1 : 4)))
+template <bool V16>
+__global__ HB_SPONGE_ATTR void leaf_hash_kernel(
     const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
     uint32_t n, size_t total, uint8_t *__restrict__ nodes, size_t node_inst_stride,
     const uint32_t *__restrict__ slens) {
@@ -338,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void leaf_hash_kernel(
     const uint32_t i = (uint32_t)(g - inst * n);
     if (slens) S = slens[inst];
     uint32_t d[8];
-    sha3_256_row(shards + inst * inst_stride + rows.off(i), S, d);
+    sha3_256_row<V16>(shards + inst * inst_stride + rows.off(i), S, d);
     store_digest(nodes + inst * node_inst_stride + (size_t)i * 32, d);
 }
 
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(kBlock) void rebuilt_list_kernel(
 
 // SHA3 of the listed rows (a grid sized for the worst case; lanes past the
 // list length exit at once, so every wave that hashes is full).
-__global__ __launch_bounds__(kBlock) void leaf_hash_list_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void leaf_hash_list_kernel(
     const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
     const uint2 *__restrict__ list, const uint32_t *__restrict__ counter,
     uint8_t *__restrict__ nodes, size_t node_inst_stride) {
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void leaf_hash_list_kernel(
     store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
 }
 
-__global__ __launch_bounds__(kBlock) void ragged_hash_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void ragged_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lens, size_t nvals, uint8_t *__restrict__ out) {
     const size_t g = blockIdx.x * (size_t)kBlock + threadIdx.x;
@@ -432,7 +436,8 @@ __global__ __launch_bounds__(kBlock) void proofs_kernel(
 
 // -------------------------------------------------------------- validate --
 // Proof::validate (merkle.rs:83-103) for proof (i, jj); see ValidateArgs.
-__global__ __launch_bounds__(kBlock) void validate_kernel(
+template <bool V16>
+__global__ HB_SPONGE_ATTR void validate_kernel(
     const uint8_t *__restrict__ values, uint32_t value_len, size_t value_inst_stride,
     RowMap vrows, uint32_t per_inst, const uint32_t *__restrict__ rows,
     const uint32_t *__restrict__ indices, const uint8_t *__restrict__ digests, uint32_t dslots,
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void validate_kernel(
     const uint32_t jj = (uint32_t)(g - inst * per_inst);
     const uint32_t r = rows ? rows[jj] : jj;
     uint32_t d[8];
-    sha3_256_row(values + inst * value_inst_stride + vrows.off(r), value_len, d);
+    sha3_256_row<V16>(values + inst * value_inst_stride + vrows.off(r), value_len, d);
     if (leaf_out) store_digest(leaf_out + inst * leaf_inst_stride + (size_t)r * 32, d);
     uint32_t i = indices ? indices[g] : r;
     uint32_t lvl_n = tree_n, used = 0;
@@ -831,6 +836,8 @@ size_t shaped_lds(size_t lanes, int max_w) {
     return (size_t)(163840 / best_w) / 512 * 512;
 }
 constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kernels (<= 128 VGPRs)
+// Grids below 2^18 sponges (< 4 waves per SIMD) take the 16-byte-load variant.
+bool few_sponges(size_t lanes) { return lanes < ((size_t)1 << 18); }
 }  // namespace
 
 uint64_t pattern_hash(const uint8_t *present, int n) {
@@ -847,9 +854,11 @@ hipError_t configure_kernels() {
     e = hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
     for (const void *k : {reinterpret_cast<const void *>(decode_matrix_kernel),
-                          reinterpret_cast<const void *>(leaf_hash_kernel),
+                          reinterpret_cast<const void *>(leaf_hash_kernel<false>),
+                          reinterpret_cast<const void *>(leaf_hash_kernel<true>),
                           reinterpret_cast<const void *>(leaf_hash_list_kernel),
-                          reinterpret_cast<const void *>(validate_kernel)}) {
+                          reinterpret_cast<const void *>(validate_kernel<false>),
+                          reinterpret_cast<const void *>(validate_kernel<true>)}) {
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
     }
@@ -940,9 +949,11 @@ hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMa
                             size_t node_inst_stride, hipStream_t s, const uint32_t *slens) {
     const size_t total = n * count;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(leaf_hash_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
-                       shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len, rows,
-                       inst_stride, (uint32_t)n, total, nodes, node_inst_stride, slens);
+    const bool v16 = few_sponges(total);
+    hipLaunchKernelGGL(v16 ? leaf_hash_kernel<true> : leaf_hash_kernel<false>,
+                       dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
+                       v16 ? 0 : shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len,
+                       rows, inst_stride, (uint32_t)n, total, nodes, node_inst_stride, slens);
     return hipGetLastError();
 }
 
@@ -996,8 +1007,10 @@ hipError_t launch_proofs(const uint8_t *nodes, size_t node_inst_stride, size_t n
 hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
     const size_t total = a.count * a.per_inst;
     if (total == 0) return hipSuccess;
-    hipLaunchKernelGGL(validate_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
-                       shaped_lds(total, kSpongeMaxWaves), s, a.values, (uint32_t)a.value_len,
+    const bool v16 = few_sponges(total);
+    hipLaunchKernelGGL(v16 ? validate_kernel<true> : validate_kernel<false>,
+                       dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
+                       v16 ? 0 : shaped_lds(total, kSpongeMaxWaves), s, a.values, (uint32_t)a.value_len,
                        a.value_inst_stride, a.vrows, (uint32_t)a.per_inst, a.rows, a.indices,
                        a.digests, (uint32_t)a.dslots, (uint32_t)a.dig_rows, a.ndig, a.roots,
                        a.root_stride, (uint32_t)a.tree_n, a.count, a.ok_out, a.leaf_out,

@@ -346,6 +346,44 @@ def test_lockstep_batched_validation(backend):
 
 
 
+def test_lockstep_batched_decodes(backend):
+    """f2: networks cranked in lockstep with every node's `decode_from_shards`
+    deferred and completed for all networks together after each round
+    (resolve_decodes; on the HIP backend one hbrbc_decode_batch launch per
+    validator count and shard length).  Outputs, fault logs and crank counts
+    equal the one-network-at-a-time run of the same seeds."""
+    # networks of one validator count and value length decode together
+    sizes = [7] * 6 + [16] * 6 + [4, 31]
+
+    def make(i, size):
+        rng = random.Random(2000 + i)
+        proposer = rng.randrange(size)
+        ids = list(range(size))
+        net = vn.VirtualNet(ids, vn.max_faulty(size),
+                            lambda j: Broadcast(j, ids, proposer, backend=backend),
+                            vn.RandomAdversary(0.2, 0.2, backend), rng, message_limit=10_000 * size)
+        return net, b"decode lockstep %03d" % i * size, proposer
+
+    seq = [make(i, s) for i, s in enumerate(sizes)]
+    for net, value, proposer in seq:
+        vn.run_broadcast(net, value, proposer)
+    st = getattr(backend, "DECODE_STATS", None)
+    before = dict(st) if st is not None else None
+    lock = [make(i, s) for i, s in enumerate(sizes)]
+    vn.run_lockstep(lock, backend, batched_decode=True)
+    outputs = 0
+    for (a, _, _), (b, _, _) in zip(seq, lock):
+        for na, nb in zip(a.nodes.values(), b.nodes.values()):
+            assert na.outputs == nb.outputs
+            assert [(f.node_id, f.kind) for f in na.faults] == [(f.node_id, f.kind) for f in nb.faults]
+            outputs += len(nb.outputs)
+        assert a.crank_count == b.crank_count
+    if st is not None:   # HIP backend: decodes went through the batched launches
+        decodes = st["decodes"] - before["decodes"]
+        launches = st["launches"] - before["launches"]
+        assert decodes >= outputs > 0 and decodes > launches > 0
+
+
 def _epoch_value(n, p):
     # ragged contributions: several proposers share a length (one batch), one
     # is empty, the rest differ

@@ -428,3 +428,59 @@ def test_baseline_sizes_roundtrip(torch_cuda, n, plen, count, erase):
         pay = r["pay"]
     sh, nd = orc.send_shards(n, f, pay[0].tobytes())
     assert np.array_equal(ref[0], sh)
+
+
+def _oracle_decode(n, leaves, root):
+    """decode_from_shards of the oracle for a list of optional shards (rse
+    rejects ragged or empty present shards before reconstructing)."""
+    lens = {len(v) for v in leaves if v is not None}
+    if len(lens) != 1 or 0 in lens:
+        return None
+    S = lens.pop()
+    arr = np.zeros((n, S), np.uint8)
+    pres = np.zeros(n, np.uint8)
+    for j, v in enumerate(leaves):
+        if v is not None:
+            arr[j] = np.frombuffer(v, np.uint8)
+            pres[j] = 1
+    return orc.decode_from_shards(n, (n - 1) // 3, arr, pres, root)[0]
+
+
+def test_decode_shards_batch_matches_decode_from_shards(torch_cuda):
+    """hbbft_amd.decode_shards_batch (deferred decodes) returns
+    exactly the oracle's decode_from_shards (broadcast.rs:563-601) per
+    request: f and worst-case erasures, too few shards, a tampered shard (root
+    mismatch), ragged shard lengths, an empty shard, a wrong root, N=1..3
+    (Coding::Trivial) -- mixed validator counts and lengths in one call."""
+    rng = np.random.default_rng(91)
+    reqs, want = [], []
+    for n, plen in [(4, 0), (4, 100), (7, 1000), (16, 4099), (16, 4099), (64, 3000), (1, 5),
+                    (2, 9), (3, 17), (10, 1)]:
+        f = (n - 1) // 3
+        k = n - 2 * f
+        pay = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+        shards, nodes = orc.send_shards(n, f, pay)
+        root = nodes[-1].tobytes()
+        rows = [shards[j].tobytes() for j in range(n)]
+        cases = []
+        gone = rng.permutation(n)[:f]
+        cases.append(([None if j in set(gone.tolist()) else rows[j] for j in range(n)], root))
+        cases.append(([rows[j] if j >= n - k else None for j in range(n)], root))
+        if n > 1:
+            cases.append(([rows[j] if j < k - 1 else None for j in range(n)], root))   # too few
+            bad = list(rows)
+            bad[0] = bytes([bad[0][0] ^ 1]) + bad[0][1:]
+            cases.append((bad, root))                                   # root mismatch
+            rag = list(rows)
+            rag[-1] = rag[-1] + b"\0"
+            cases.append((rag, root))                                   # IncorrectShardSize
+        cases.append((rows, bytes(32)))                                 # wrong root
+        for leaves, r in cases:
+            reqs.append((n, leaves, r))
+            want.append(_oracle_decode(n, leaves, r))
+    reqs.append((4, [b"", b"", b"", b""], bytes(32)))                   # EmptyShard
+    want.append(None)
+    got = hb.decode_shards_batch(reqs)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, reqs[i][0])
+    assert any(w is not None for w in want) and any(w is None for w in want)

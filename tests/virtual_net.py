@@ -18,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from hbbft_amd.broadcast import Broadcast, Message, broadcast_many, prevalidate  # noqa: E402
+from hbbft_amd.broadcast import (Broadcast, Message, broadcast_many, prevalidate,  # noqa: E402
+                                 resolve_decodes)
 
 
 class CrankError(AssertionError):
@@ -254,7 +255,7 @@ def check_outcome(net, value, proposer_id):
     return net
 
 
-def run_lockstep(items, backend, batched_input=False):
+def run_lockstep(items, backend, batched_input=False, batched_decode=False):
     """Many broadcast networks cranked in lockstep, one crank per network per
     round.  Before every round the Value / Echo proofs all networks queued
     since the previous round are validated together, one batched launch per
@@ -263,7 +264,19 @@ def run_lockstep(items, backend, batched_input=False):
     RNG and state, so outcomes equal those of `run_broadcast`.
     batched_input: the proposers' inputs go through `broadcast_many` (one
     frame+encode+tree launch per size) instead of one
-    `send_input` each.  items: [(net, value, proposer)]."""
+    `send_input` each.
+    batched_decode: every node defers `decode_from_shards` to a shared sink
+    and the decodes of all networks are completed together after each round
+    (hbbft_amd.broadcast.resolve_decodes: one launch per validator count and
+    shard length); a node handles one message per round, so
+    its decode completes before its next message.  items: [(net, value,
+    proposer)]."""
+    sink, owner = [], {}
+    if batched_decode:
+        for net, _, _ in items:
+            for nid, nd in net.nodes.items():
+                nd.algo.decode_sink = sink
+                owner[id(nd.algo)] = (net, nid)
     if batched_input:
         steps = broadcast_many([(net.nodes[p].algo, v) for net, v, p in items], backend)
         for (net, _, proposer), step in zip(items, steps):
@@ -288,6 +301,10 @@ def run_lockstep(items, backend, batched_input=False):
                 continue
             net.crank_expect()
             nxt.append(it)
+        for bc, step in resolve_decodes(sink, backend):
+            net, nid = owner[id(bc)]
+            net.process_step(nid, step)
+        sink.clear()
         live = nxt
     for net, value, proposer in items:
         check_outcome(net, value, proposer)
