@@ -1,61 +1,103 @@
 #!/usr/bin/env python3
-"""Per-kernel HBM traffic from two rocprofv3 counter passes (FETCH_SIZE and
-WRITE_SIZE, separate runs as MI355X_MICROARCH.md prescribes) of
-`bench.py --steps 1 --warmup 1`.
+"""Per-kernel HBM traffic and Keccak VALU ops from rocprofv3 counter passes
+(FETCH_SIZE, WRITE_SIZE and SQ_INSTS_VALU, each its own run as
+MI355X_MICROARCH.md prescribes) of `bench.py --steps 1 --warmup 1`, as
+collected by tools/profile.sh.
 
 FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports half the bytes
-of a wide streaming read, so it is doubled.  Output: bytes per launch and per
-instance for every hbrbc kernel, and the "cfg:stage" -> bytes-per-instance map
-bench.py reads for roofline.traffic.
+of a wide streaming read, so it is doubled.  Output (out.json): bytes per
+launch and per instance for every hbrbc kernel of every profiled config, and
+the "cfg:stage" -> bytes-per-instance map bench.py reads for roofline.traffic.
+With an SQ pass and a sponge geometry it also writes
+profiles/valu_ops_per_perm.json: 32-bit lane-ops per Keccak-f[1600] of the
+leaf-hash kernel = SQ_INSTS_VALU x 64 / permutations per launch.
 
-usage: pmc_traffic.py <profile dir> <config> <instances per launch> <out.json>
+usage: pmc_traffic.py <out.json> <profile dir>:<config>:<instances per launch>
+                      [:<n>:<shard_len>] ...
 """
 import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
 
 STAGE = {"leaf_hash_kernel": "leaf_hash", "validate_kernel": "validate", "frame_kernel": "frame",
          "unframe_kernel": "unframe", "tree_level_kernel": "tree_levels", "proofs_kernel": "proofs",
-         "decode_matrix_kernel": "decode_matrix"}
+         "decode_matrix_kernel": "decode_matrix", "decode_check_kernel": "decode_check",
+         "gf_bitslice_kernel": "reconstruct"}
 
 
 def kname(n):
-    m = re.search(r"(hbrbc_enc_\w+|\w+_kernel(<[^>]*>)?)", n)
+    m = re.search(r"(hbrbc_(?:enc|dec)_\w+|\w+_kernel(<[^>]*>)?)", n)
     return m.group(1) if m else n[:40]
 
 
-def per_launch(path, counter):
-    f = glob.glob(path + "/**/run_counter_collection.csv", recursive=True)[0]
+def base(k):
+    return k.split("<")[0]
+
+
+def per_launch(path, counter, scale):
+    fs = glob.glob(path + "*/**/run_counter_collection.csv", recursive=True)
+    if not fs:
+        return {}
     tot, cnt = collections.defaultdict(float), collections.defaultdict(set)
-    for x in csv.DictReader(open(f)):
+    for x in csv.DictReader(open(fs[0])):
         if "hbrbc" not in x["Kernel_Name"] or x["Counter_Name"] != counter:
             continue
         k = kname(x["Kernel_Name"])
-        tot[k] += float(x["Counter_Value"]) * 1024.0
+        tot[k] += float(x["Counter_Value"]) * scale
         cnt[k].add(x["Dispatch_Id"])
     return {k: tot[k] / len(cnt[k]) for k in tot}
 
 
 def main():
-    d, cfg, inst, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    fe, wr = per_launch(d + "/pmc_fetch", "FETCH_SIZE"), per_launch(d + "/pmc_write", "WRITE_SIZE")
-    kernels = {}
-    for k in sorted(set(fe) | set(wr)):
-        f2 = 2.0 * fe.get(k, 0.0)
-        kernels[k] = {"fetch_raw_bytes": fe.get(k, 0.0), "fetch_corrected_bytes": f2,
-                      "write_bytes": wr.get(k, 0.0), "hbm_bytes": f2 + wr.get(k, 0.0),
-                      "hbm_bytes_per_instance": (f2 + wr.get(k, 0.0)) / inst}
-    traffic = {"%s:%s" % (cfg, STAGE[k]): v["hbm_bytes_per_instance"]
-               for k, v in kernels.items() if k in STAGE}
-    for k, v in kernels.items():
-        if k.startswith("hbrbc_enc_") or k.startswith("gf_bitslice_kernel<14"):
-            traffic["%s:encode" % cfg] = v["hbm_bytes_per_instance"]
+    out = sys.argv[1]
+    try:
+        doc = json.load(open(out))
+    except (OSError, ValueError):
+        doc = {}
+    kernels_all, traffic = doc.get("kernels", {}), doc.get("traffic", {})
+    for spec in sys.argv[2:]:
+        parts = spec.split(":")
+        d, cfg, inst = parts[0], parts[1], int(parts[2])
+        fe = per_launch(d + "/pmc_fetch", "FETCH_SIZE", 1024.0)
+        wr = per_launch(d + "/pmc_write", "WRITE_SIZE", 1024.0)
+        kernels = {}
+        for k in sorted(set(fe) | set(wr)):
+            f2 = 2.0 * fe.get(k, 0.0)
+            kernels[k] = {"fetch_raw_bytes": fe.get(k, 0.0), "fetch_corrected_bytes": f2,
+                          "write_bytes": wr.get(k, 0.0), "hbm_bytes": f2 + wr.get(k, 0.0),
+                          "hbm_bytes_per_instance": (f2 + wr.get(k, 0.0)) / inst}
+        kernels_all[cfg] = kernels
+        # a stage = the sum of its kernels (the specialised encoder / decoder
+        # programs of one matrix run one after another on the same rows)
+        stage_bytes = collections.defaultdict(float)
+        for k, v in kernels.items():
+            if base(k) in STAGE:
+                stage_bytes[STAGE[base(k)]] += v["hbm_bytes_per_instance"]
+            elif k.startswith("hbrbc_enc_"):
+                stage_bytes["encode"] += v["hbm_bytes_per_instance"]
+            elif k.startswith("hbrbc_dec_"):
+                stage_bytes["reconstruct"] += v["hbm_bytes_per_instance"]
+        for st, b in stage_bytes.items():
+            traffic["%s:%s" % (cfg, st)] = b
+        if len(parts) >= 5:
+            n, S = int(parts[3]), int(parts[4])
+            sq = per_launch(d + "/pmc_sq", "SQ_INSTS_VALU", 1.0)
+            leaf = [v for k, v in sq.items() if base(k) == "leaf_hash_kernel"]
+            if leaf:
+                perms = inst * n * ((S + 1 + 135) // 136)
+                ops = leaf[0] * 64.0 / perms
+                json.dump({"leaf_hash_kernel": ops, "source": "%s, %s: SQ_INSTS_VALU %.0f x 64 / "
+                           "%d permutations per launch" % (os.path.basename(d), cfg, leaf[0], perms)},
+                          open(os.path.join(os.path.dirname(out), "valu_ops_per_perm.json"), "w"),
+                          indent=1)
+                print("leaf_hash lane-ops per permutation: %.1f" % ops)
     traffic["_note"] = ("HBM bytes per instance per launch: (2 x FETCH_SIZE + WRITE_SIZE) x 1024 "
-                        "/ %d instances; source %s" % (inst, d))
-    json.dump({"kernels": kernels, "traffic": traffic}, open(out, "w"), indent=1)
+                        "/ instances per launch (rocprofv3 --pmc passes, tools/profile.sh)")
+    json.dump({"kernels": kernels_all, "traffic": traffic}, open(out, "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
 
