@@ -11,7 +11,7 @@ if [ -z "$SETS" ]; then
 fi
 for c in ${CONFIGS:-cfg3}; do
   for s in ${SETS}; do
-    tag=$(echo "$s" | tr ',=' '__')
+    tag=$(echo "$s" | tr ',=/.' '____')
     log=gpurun_out/ab/${c}_${tag}.log
     env $(echo "$s" | tr ',' ' ') timeout -k 10 300 python bench.py --config $c --steps ${STEPS:-4} --warmup 1 --no-cpu --mode ${MODE:-instances} > $log 2>&1
     rc=$?
@@ -21,7 +21,7 @@ l=[x for x in open('$log') if x.startswith('{')]
 if not l: print('$c $s rc=$rc', open('$log').read()[-800:])
 else:
   d=json.loads(l[-1]); st=d['stages_ms_per_step']
-  print('$c $s  %.2f GB/s  %.2f ms/step  encode %.2f  reconstruct %.2f' % (d['value'], d['ms_per_step'], st['encode'], st['reconstruct']))
+  print('$c $s  %.2f GB/s  %.2f ms/step  encode %.2f  reconstruct %.2f  leaf %.2f  validate %.2f' % (d['value'], d['ms_per_step'], st['encode'], st['reconstruct'], st['leaf_hash'], st['validate']))
 "
     case $rc in 0) ;; *) exit $rc;; esac
   done
