@@ -560,7 +560,16 @@ def main():
         head = run_instances(args, n, plen, count, erase, rank, world, dev, local)
     if args.mode in ("validators", "both"):
         torch.cuda.empty_cache()
-        vobj = run_validators(args, n, plen, vcount, rank, world, dev, local)
+        if head is None:
+            vobj = run_validators(args, n, plen, vcount, rank, world, dev, local)
+        else:
+            # the headline is measured: a failure of the (secondary) validator
+            # simulation is reported in the line instead of losing it
+            try:
+                vobj = run_validators(args, n, plen, vcount, rank, world, dev, local)
+            except Exception as e:  # noqa: BLE001
+                vobj = {"error": "%s: %s" % (type(e).__name__, e)}
+                print("bench: validator-sharded run failed: %r" % (e,), file=sys.stderr)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -579,7 +588,7 @@ def main():
                 "stages_ms_per_step": head["stages_ms_per_step"],
             }
             if vobj is not None:
-                if cpu is not None:
+                if cpu is not None and "error" not in vobj:
                     vobj["cpu_baseline"] = dict(cpu, note="the same per-instance pipeline; the "
                                                 "CPU leg decodes each instance once")
                 line["validators"] = vobj
