@@ -196,10 +196,29 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
         except (ValueError, OSError):
             traffic = None
     step_bytes = sum(alg[s] * (stages[s][1] / max(steps, 1)) for s in stages if s in alg)
+    # every stage's HBM view (algorithmic bytes per launch / live launch time),
+    # with the PMC traffic ratio where a counter pass exists for this config
+    per_stage = {}
+    pm_all = {}
+    if os.path.exists(prof):
+        try:
+            pm_all = json.load(open(prof)).get("traffic", {})
+        except (ValueError, OSError):
+            pm_all = {}
+    for s_, (ms_, nl_) in live.items():
+        if s_ not in alg or nl_ == 0:
+            continue
+        tl = ms_ / 1e3 / nl_
+        e = {"ms_per_launch": tl * 1e3, "alg_bytes_per_launch": alg[s_],
+             "achieved_GBps": alg[s_] / tl / 1e9, "hbm_frac": alg[s_] / tl / 1e9 / HBM_PEAK_GBS}
+        key = "%s:%s" % (config, s_)
+        if key in pm_all and alg[s_] > 0:
+            e["traffic_over_alg"] = pm_all[key] * per_launch / alg[s_]
+        per_stage[s_] = e
     r = {"kernel": dom, "launch_ms": t * 1e3, "traffic": traffic,
          "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": hbm_gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg[dom]},
-         "pipeline_alg_bytes_per_step": step_bytes,
+         "pipeline_alg_bytes_per_step": step_bytes, "stages": per_stage,
          "pipeline_hbm_frac": step_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS}
     if dom in perms:
         opp, src = valu_ops_per_perm()

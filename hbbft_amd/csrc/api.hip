@@ -409,9 +409,26 @@ PatternCache cache_view(hbrbc_ctx *c) {
 
 // Leaf hashes + all levels into a node slab (known_leaves: level 0 holds the
 // leaves of every row but the ones the last reconstruct rebuilt).
+// Leaf kernel + one launch per level (default), or leaves and levels in one
+// launch with the levels reduced in LDS (HBRBC_MERKLE_FUSED=1).  The fused
+// form measured slower at cfg3 (leaf hash + levels 20.95 -> 21.4 ms per step:
+// each workgroup holds its four wave slots through six dependent pair-hash
+// levels with at most half its lanes busy) and flat at cfg5.
+bool merkle_split() {
+    const char *e = getenv("HBRBC_MERKLE_FUSED");
+    return !(e && !std::strcmp(e, "1"));
+}
+
 int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, const RowMap &rows,
                size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
                size_t node_inst_stride, bool known_leaves, hipStream_t s) {
+    if (!known_leaves && merkle_fused_ok(n) && !merkle_split()) {
+        // leaves and levels in one launch, attributed to the leaf-hash stage
+        StageTimer t(c, HBRBC_STAGE_LEAF_HASH, s);
+        HB_HIP(launch_merkle_fused(shards, shard_len, rows, inst_stride, n, count, nodes,
+                                   node_inst_stride, s));
+        return HBRBC_OK;
+    }
     {
         StageTimer t(c, HBRBC_STAGE_LEAF_HASH, s);
         if (!known_leaves) {
@@ -1116,6 +1133,12 @@ int hbrbc_merkle_ragged(hbrbc_ctx *c, const uint8_t *shards, const uint32_t *sha
     if (st) return st;
     HB_HIP(hipSetDevice(c->device));
     hipStream_t s = pick(c, stream);
+    if (merkle_fused_ok(c->n) && !merkle_split()) {
+        StageTimer t(c, HBRBC_STAGE_LEAF_HASH, s);
+        HB_HIP(launch_merkle_fused(shards, shard_stride, plain_rows(shard_stride), inst_stride,
+                                   c->n, count, nodes, node_inst_stride, s, shard_lens));
+        return HBRBC_OK;
+    }
     {
         StageTimer t(c, HBRBC_STAGE_LEAF_HASH, s);
         HB_HIP(launch_leaf_hash(shards, shard_stride, plain_rows(shard_stride), inst_stride, c->n,

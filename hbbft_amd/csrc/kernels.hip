@@ -346,6 +346,55 @@ __global__ HB_SPONGE_ATTR void leaf_hash_kernel(
     store_digest(nodes + inst * node_inst_stride + (size_t)i * 32, d);
 }
 
+// Leaf hashes and every level of whole trees in one launch (north_star:
+// "Merkle levels reduced in LDS"): lane = (instance li of the block, leaf);
+// after the sponges the leaf digests go to level 0 of the node slab and to
+// LDS, then each level is one pair hash per lane, read from one LDS buffer and
+// written to the other and to the slab (merkle.rs:20-33, 128-140: an odd last
+// node is promoted unchanged).  A block holds ipb = 256 / n whole instances.
+template <bool V16>
+__global__ HB_SPONGE_ATTR void merkle_tree_kernel(
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride, uint32_t n,
+    uint32_t ipb, size_t count, uint8_t *__restrict__ nodes, size_t node_inst_stride,
+    const uint32_t *__restrict__ slens) {
+    __shared__ uint4 lvl[2][kBlock][2];   // two levels of 256 digests: 16 KB
+    const uint32_t li = threadIdx.x / n, leaf = threadIdx.x - li * n;
+    const size_t inst = (size_t)blockIdx.x * ipb + li;
+    const bool active = li < ipb && inst < count;   // no early exit: every lane meets every barrier
+    uint8_t *ns = nodes + inst * node_inst_stride;
+    if (active) {
+        uint32_t d[8];
+        sha3_256_row<V16>(shards + inst * inst_stride + rows.off(leaf), slens ? slens[inst] : S, d);
+        store_digest(ns + (size_t)leaf * 32, d);
+        lvl[0][threadIdx.x][0] = make_uint4(d[0], d[1], d[2], d[3]);
+        lvl[0][threadIdx.x][1] = make_uint4(d[4], d[5], d[6], d[7]);
+    }
+    const uint32_t base = li * n;   // this instance's slots in each level buffer
+    uint32_t off = 0, sz = n, cur = 0;
+    while (sz > 1) {                // the same trip count in every lane
+        __syncthreads();
+        const uint32_t nsz = (sz + 1) >> 1;
+        if (active && leaf < nsz) {
+            const uint4 a0 = lvl[cur][base + 2 * leaf][0], a1 = lvl[cur][base + 2 * leaf][1];
+            uint32_t a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}, o[8];
+            if (2 * leaf + 1 < sz) {
+                const uint4 b0 = lvl[cur][base + 2 * leaf + 1][0], b1 = lvl[cur][base + 2 * leaf + 1][1];
+                const uint32_t b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                sha3_256_pair(a, b, o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) o[w] = a[w];
+            }
+            store_digest(ns + (size_t)(off + sz + leaf) * 32, o);
+            lvl[cur ^ 1][base + leaf][0] = make_uint4(o[0], o[1], o[2], o[3]);
+            lvl[cur ^ 1][base + leaf][1] = make_uint4(o[4], o[5], o[6], o[7]);
+        }
+        off += sz;
+        sz = nsz;
+        cur ^= 1u;
+    }
+}
+
 // The rows a reconstruct rebuilt, compacted into one list: entry e = (instance,
 // row).  One thread per instance appends its slot's out_idx rows.
 __global__ __launch_bounds__(kBlock) void rebuilt_list_kernel(
@@ -818,7 +867,7 @@ int g_num_cus = 256;
 // lanes at 5 waves/SIMD = 1.6 rounds, 80 % busy).  Pick the waves/SIMD in
 // [2, max_w] whose rounds are fullest and enforce it with dynamic LDS (one
 // 256-thread block = one wave per SIMD, so blocks/CU = waves/SIMD).
-size_t shaped_lds(size_t lanes, int max_w) {
+size_t shaped_lds(size_t lanes, int max_w, size_t static_lds = 0) {
     const size_t per_w = (size_t)g_num_cus * kBlock;
     if (lanes >= per_w * (size_t)max_w * 8) return 0;  // many rounds: the tail is small
     int best_w = max_w;
@@ -833,7 +882,7 @@ size_t shaped_lds(size_t lanes, int max_w) {
         }
     }
     if (best_w == max_w) return 0;
-    return (size_t)(163840 / best_w) / 512 * 512;
+    return (size_t)(163840 / best_w - static_lds) / 512 * 512;
 }
 constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kernels (<= 128 VGPRs)
 // Grids below 2^18 sponges (< 4 waves per SIMD) take the 16-byte-load variant.
@@ -857,9 +906,17 @@ hipError_t configure_kernels() {
                           reinterpret_cast<const void *>(leaf_hash_kernel<false>),
                           reinterpret_cast<const void *>(leaf_hash_kernel<true>),
                           reinterpret_cast<const void *>(leaf_hash_list_kernel),
+
                           reinterpret_cast<const void *>(validate_kernel<false>),
                           reinterpret_cast<const void *>(validate_kernel<true>)}) {
         e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+    }
+    // (static LDS counts against the same 160 KB)
+    for (const void *k : {reinterpret_cast<const void *>(merkle_tree_kernel<false>),
+                          reinterpret_cast<const void *>(merkle_tree_kernel<true>)}) {
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024 - 2 * kBlock * 32);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -954,6 +1011,27 @@ hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMa
                        dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
                        v16 ? 0 : shaped_lds(total, kSpongeMaxWaves), s, shards, (uint32_t)shard_len,
                        rows, inst_stride, (uint32_t)n, total, nodes, node_inst_stride, slens);
+    return hipGetLastError();
+}
+
+bool merkle_fused_ok(size_t n) {
+    // whole instances per 256-lane block, at most 1/16 of the lanes idle
+    return n >= 2 && n <= (size_t)kBlock && (kBlock % n) * 16 <= (size_t)kBlock;
+}
+
+hipError_t launch_merkle_fused(const uint8_t *shards, size_t shard_len, const RowMap &rows,
+                               size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
+                               size_t node_inst_stride, hipStream_t s, const uint32_t *slens) {
+    if (count == 0) return hipSuccess;
+    if (!merkle_fused_ok(n)) return hipErrorInvalidValue;
+    const size_t ipb = kBlock / n;
+    const size_t blocks = (count + ipb - 1) / ipb;
+    if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const bool v16 = few_sponges(count * n);
+    const size_t dyn = v16 ? 0 : shaped_lds(blocks * kBlock, kSpongeMaxWaves, 2 * kBlock * 32);
+    hipLaunchKernelGGL(v16 ? merkle_tree_kernel<true> : merkle_tree_kernel<false>, dim3((unsigned)blocks),
+                       dim3(kBlock), dyn, s, shards, (uint32_t)shard_len, rows, inst_stride,
+                       (uint32_t)n, (uint32_t)ipb, count, nodes, node_inst_stride, slens);
     return hipGetLastError();
 }
 

@@ -82,6 +82,13 @@ hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMa
                             size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
                             size_t node_inst_stride, hipStream_t s,
                             const uint32_t *slens = nullptr);
+// Leaf hashes and all tree levels in one launch (LDS level reduction); only
+// for validator counts with merkle_fused_ok(n).
+bool merkle_fused_ok(size_t n);
+hipError_t launch_merkle_fused(const uint8_t *shards, size_t shard_len, const RowMap &rows,
+                               size_t inst_stride, size_t n, size_t count, uint8_t *nodes,
+                               size_t node_inst_stride, hipStream_t s,
+                               const uint32_t *slens = nullptr);
 // SHA3 of only the rows a reconstruct rebuilt (out_idx of each instance's
 // decode-matrix slot) -> their level-0 nodes; the other leaves are already
 // there (decode with known leaves).

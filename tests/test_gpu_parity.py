@@ -121,6 +121,32 @@ def test_merkle_ragged_values_vs_oracle(torch_cuda):
         assert [d for level in lv for d in level] == [r.tobytes() for r in ref]
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_merkle_batch_level_forms_vs_oracle(torch_cuda, monkeypatch, fused):
+    """hbrbc_merkle_batch with one launch per level (default) and with the
+    leaves and levels in one launch, levels reduced in LDS
+    (HBRBC_MERKLE_FUSED=1; whole instances per 256-lane block, odd nodes
+    promoted): every node of every tree equals the oracle's, for validator
+    counts that fill a block exactly, nearly, or not at all (fallback)."""
+    torch = torch_cuda
+    monkeypatch.setenv("HBRBC_MERKLE_FUSED", fused)
+    rng = np.random.default_rng(17)
+    for n, L, count in [(2, 5, 3), (4, 300, 5), (7, 136, 9), (16, 1000, 17), (64, 2000, 5),
+                        (100, 77, 3), (128, 513, 3), (250, 40, 2), (256, 272, 2)]:
+        rb = hb.RbcBatch(n, device=0)
+        stride = (L + 15) // 16 * 16
+        data = rng.integers(0, 256, (count, n, stride), dtype=np.uint8)
+        slab = torch.from_numpy(data).cuda()
+        nodes = rb.alloc_nodes(count)
+        nodes.fill_(0xEE)
+        rb.merkle(slab, L, nodes)
+        torch.cuda.synchronize()
+        got = nodes.cpu().numpy()
+        for i in range(count):
+            ref = orc.merkle_build([data[i, j, :L].tobytes() for j in range(n)])
+            assert np.array_equal(got[i], ref), (fused, n, i)
+
+
 def test_sha3_rate_boundaries_golden(torch_cuda):
     kat = load("sha3_kat.json")
     vals = [bytes((7 * i + 3) & 0xFF for i in range(L)) for L in range(301)]
