@@ -128,6 +128,11 @@ def lib():
         "hbrbc_jit_decode_groups": (_S, [_S, _S, _P]),
         "hbrbc_jit_build_decode": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p]),
         "hbrbc_jit_decode_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p, _S]),
+        "hbrbc_pairing_workspace_size": (_S, [_S]),
+        "hbrbc_pairing_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P, _P]),
+        "hbrbc_pairing_check_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P]),
+        "hbrbc_pairing_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                               ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

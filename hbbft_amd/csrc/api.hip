@@ -1854,4 +1854,70 @@ const char *hbrbc_stage_name(int stage) {
     return (stage >= 0 && stage < HBRBC_STAGE_COUNT) ? names[stage] : "?";
 }
 
+// ---- threshold-decrypt share verification (pairing.hip) ----
+size_t hbrbc_pairing_workspace_size(size_t pairings) {
+    return round_up(pairings * 576, 256) + round_up(pairings, 256);
+}
+
+static int pairing_run(const uint8_t *g1, const uint8_t *g2, size_t n_pair, size_t n_out,
+                       int per_out, uint8_t *gt_out, uint8_t *ok_out, uint8_t *status_out,
+                       void *workspace, hipStream_t s) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(HBRBC_E_NO_DEVICE, "no HIP device visible");
+    uint32_t *ws = static_cast<uint32_t *>(workspace);
+    uint8_t *st = static_cast<uint8_t *>(workspace) + round_up(n_pair * 576, 256);
+    HB_HIP(launch_pairing_miller(g1, 96, g2, 192, n_pair, per_out == 2, ws, st, s));
+    if (status_out) HB_HIP(hipMemcpyAsync(status_out, st, n_pair, hipMemcpyDeviceToDevice, s));
+    HB_HIP(launch_pairing_final(ws, n_pair, n_out, per_out, st, gt_out, ok_out, s));
+    return HBRBC_OK;
+}
+
+int hbrbc_pairing_batch(const uint8_t *g1, const uint8_t *g2, size_t count, uint8_t *gt_out,
+                        uint8_t *status_out, void *workspace, void *stream) {
+    if (count == 0) return HBRBC_OK;
+    if (!g1 || !g2 || !gt_out || !workspace) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    return pairing_run(g1, g2, count, count, 1, gt_out, nullptr, status_out, workspace,
+                       static_cast<hipStream_t>(stream));
+}
+
+int hbrbc_pairing_check_batch(const uint8_t *g1, const uint8_t *g2, size_t count,
+                              uint8_t *ok_out, void *workspace, void *stream) {
+    if (count == 0) return HBRBC_OK;
+    if (!g1 || !g2 || !ok_out || !workspace) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    return pairing_run(g1, g2, 2 * count, count, 2, nullptr, ok_out, nullptr, workspace,
+                       static_cast<hipStream_t>(stream));
+}
+
+int hbrbc_pairing_check(const uint8_t a[96], const uint8_t b[192], const uint8_t c[96],
+                        const uint8_t d[192], int *result) {
+    if (!a || !b || !c || !d || !result) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(HBRBC_E_NO_DEVICE, "no HIP device visible");
+    const size_t ws_bytes = hbrbc_pairing_workspace_size(2);
+    const size_t total = 2 * 96 + 2 * 192 + 16 + ws_bytes;
+    uint8_t *dev = nullptr;
+    HB_HIP(hipMalloc(&dev, total));
+    std::vector<uint8_t> host(2 * 96 + 2 * 192);
+    memcpy(host.data(), a, 96);
+    memcpy(host.data() + 96, c, 96);
+    memcpy(host.data() + 192, b, 192);
+    memcpy(host.data() + 384, d, 192);
+    uint8_t ok = 0;
+    int rc = HBRBC_OK;
+    hipError_t e = hipMemcpy(dev, host.data(), host.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        rc = pairing_run(dev, dev + 192, 2, 1, 2, nullptr, dev + 576, nullptr, dev + 592,
+                         nullptr);
+        if (rc == HBRBC_OK) e = hipMemcpy(&ok, dev + 576, 1, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(dev);
+    if (e != hipSuccess) return fail(HBRBC_E_DEVICE, "pairing check: %s", hipGetErrorString(e));
+    if (rc != HBRBC_OK) return rc;
+    if (ok == 2) return fail(HBRBC_E_INVALID_ARG, "invalid curve point");
+    *result = ok;
+    return HBRBC_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,760 @@
+// pairing.hip -- batched BLS12-381 pairing checks for threshold-decrypt share
+// verification.
+//
+// Reference: /root/reference/src/threshold_decrypt.rs:142 (`ct.verify()`) and
+// :220-228 (`pk.verify_decryption_share(share, ct)`), both in `threshold_crypto`
+// (git rev 624eeee, Cargo.toml:36), which evaluate
+//
+//     Ciphertext::verify                   e(G1::one(), W) == e(U, H)
+//     PublicKeyShare::verify_decryption_share  e(share, H) == e(pk_i, W)
+//
+// with H = hash_g1_g2(U, V) and `PEngine::pairing` = the `pairing` crate's
+// BLS12-381 optimal ate pairing.  A check here is e(a, b) == e(c, d),
+// evaluated as one final exponentiation of f_a,b * f_-c,d (the two GT values
+// are equal iff that product exponentiates to 1; GT has prime order r).
+//
+// MI355X layout.  One lane owns one Miller loop (kernel 1) or one final
+// exponentiation (kernel 2): the arithmetic is serial 381-bit Montgomery
+// products on 12 x 32-bit limbs (v_mad_u64_u32 chains), so a lane-per-pairing
+// mapping keeps every limb in VGPRs with no cross-lane traffic.  The Miller
+// values travel between the kernels in a limb-major workspace
+// ([144 words][pairings]), so every store and load is one coalesced dword per
+// lane.  Points arrive in the crate's uncompressed encodings (G1 96 bytes
+// x || y, G2 192 bytes x.c1 || x.c0 || y.c1 || y.c0, big-endian, flag bits
+// in byte 0) and are checked for canonical coordinates and curve membership;
+// subgroup membership is the caller's (the crate's deserialisation enforces it).
+//
+// Tower: Fp2 = Fp[u]/(u^2+1), Fp6 = Fp2[v]/(v^3 - (u+1)), Fp12 = Fp6[w]/(w^2 - v),
+// the crate's.  Miller loop over |x| = 0xd201000000010000 with homogeneous
+// projective doubling/addition on the M-type twist y^2 = x^3 + 4(u+1); each
+// line is scaled into the sparse form (c0, c1, c4) and applied with
+// mul_by_014; f is conjugated at the end (x < 0).  Final exponentiation: easy
+// part, then the crate's hard-part chain (= f^(3 (p^4 - p^2 + 1)/r)).
+#include "bls_consts.hpp"
+#include "device_common.hpp"
+#include "launchers.hpp"
+
+namespace hbrbc {
+
+namespace {
+
+using namespace bls;
+
+constexpr int NL = 12;  // 32-bit limbs per Fp element
+
+struct Fp { uint32_t l[NL]; };
+struct Fp2 { Fp c0, c1; };
+struct Fp6 { Fp2 c0, c1, c2; };
+struct Fp12 { Fp6 c0, c1; };
+
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- Fp
+DEV void fp_set(Fp &r, const uint32_t (&v)[NL]) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) r.l[i] = v[i];
+}
+
+DEV void fp_zero(Fp &r) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) r.l[i] = 0;
+}
+
+DEV bool fp_is_zero(const Fp &a) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) t |= a.l[i];
+    return t == 0;
+}
+
+DEV bool fp_eq(const Fp &a, const Fp &b) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) t |= a.l[i] ^ b.l[i];
+    return t == 0;
+}
+
+// r = t - p if t >= p else t  (t < 2p)
+DEV void fp_reduce_once(Fp &r, const uint32_t (&t)[NL]) {
+    uint32_t s[NL];
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const uint64_t d = (uint64_t)t[i] - kP[i] - br;
+        s[i] = (uint32_t)d;
+        br = (d >> 32) & 1u;
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) r.l[i] = br ? t[i] : s[i];
+}
+
+DEV void fp_add(Fp &r, const Fp &a, const Fp &b) {
+    uint32_t t[NL];
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        c += (uint64_t)a.l[i] + b.l[i];
+        t[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    fp_reduce_once(r, t);  // a + b < 2p < 2^382: no carry out of limb 11
+}
+
+DEV void fp_sub(Fp &r, const Fp &a, const Fp &b) {
+    uint32_t t[NL];
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const uint64_t d = (uint64_t)a.l[i] - b.l[i] - br;
+        t[i] = (uint32_t)d;
+        br = (d >> 32) & 1u;
+    }
+    const uint32_t mask = 0u - (uint32_t)br;  // add p back on borrow
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        c += (uint64_t)t[i] + (kP[i] & mask);
+        r.l[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+
+DEV void fp_dbl(Fp &r, const Fp &a) { fp_add(r, a, a); }
+
+DEV void fp_neg(Fp &r, const Fp &a) {
+    Fp z;
+    fp_zero(z);
+    fp_sub(r, z, a);
+}
+
+// Montgomery product a*b*2^-384 mod p, CIOS over 32-bit limbs.  p < 2^381,
+// so the running value stays below 2p < 2^382 and one extra word holds every
+// carry (the top limb of p leaves three spare bits).
+DEV void fp_mul(Fp &r, const Fp &a, const Fp &b) {
+    uint32_t t[NL + 1];
+#pragma unroll
+    for (int i = 0; i <= NL; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            c = (uint64_t)a.l[j] * b.l[i] + t[j] + (c >> 32);
+            t[j] = (uint32_t)c;
+        }
+        t[NL] += (uint32_t)(c >> 32);
+        const uint32_t m = t[0] * kInv32;
+        c = (uint64_t)m * kP[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < NL; ++j) {
+            c = (uint64_t)m * kP[j] + t[j] + (c >> 32);
+            t[j - 1] = (uint32_t)c;
+        }
+        c = (uint64_t)t[NL] + (c >> 32);
+        t[NL - 1] = (uint32_t)c;
+        t[NL] = (uint32_t)(c >> 32);
+    }
+    uint32_t u[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) u[i] = t[i];
+    fp_reduce_once(r, u);
+}
+
+DEV void fp_sqr(Fp &r, const Fp &a) { fp_mul(r, a, a); }
+
+// a^(p-2) (Fermat); once per final exponentiation.
+__device__ __noinline__ void fp_inv(Fp &r, const Fp &a) {
+    Fp acc, base = a;
+    fp_set(acc, kOne);
+    for (int w = 0; w < NL; ++w) {
+        uint32_t e = kPminus2[w];
+        for (int b = 0; b < 32; ++b) {
+            if (e & 1u) fp_mul(acc, acc, base);
+            fp_sqr(base, base);
+            e >>= 1;
+        }
+    }
+    r = acc;
+}
+
+// ---------------------------------------------------------------- Fp2
+DEV void fp2_add(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp_add(r.c0, a.c0, b.c0); fp_add(r.c1, a.c1, b.c1); }
+DEV void fp2_sub(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp_sub(r.c0, a.c0, b.c0); fp_sub(r.c1, a.c1, b.c1); }
+DEV void fp2_dbl(Fp2 &r, const Fp2 &a) { fp_dbl(r.c0, a.c0); fp_dbl(r.c1, a.c1); }
+DEV void fp2_neg(Fp2 &r, const Fp2 &a) { fp_neg(r.c0, a.c0); fp_neg(r.c1, a.c1); }
+DEV void fp2_conj(Fp2 &r, const Fp2 &a) { r.c0 = a.c0; fp_neg(r.c1, a.c1); }
+DEV void fp2_zero(Fp2 &r) { fp_zero(r.c0); fp_zero(r.c1); }
+DEV bool fp2_is_zero(const Fp2 &a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+DEV bool fp2_eq(const Fp2 &a, const Fp2 &b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+
+__device__ __noinline__ void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+    Fp t0, t1, s0, s1;
+    fp_mul(t0, a.c0, b.c0);
+    fp_mul(t1, a.c1, b.c1);
+    fp_add(s0, a.c0, a.c1);
+    fp_add(s1, b.c0, b.c1);
+    fp_mul(s0, s0, s1);
+    fp_sub(r.c0, t0, t1);
+    fp_sub(s0, s0, t0);
+    fp_sub(r.c1, s0, t1);
+}
+
+__device__ __noinline__ void fp2_sqr(Fp2 &r, const Fp2 &a) {
+    Fp s, d, m;
+    fp_add(s, a.c0, a.c1);
+    fp_sub(d, a.c0, a.c1);
+    fp_mul(m, a.c0, a.c1);
+    fp_mul(r.c0, s, d);
+    fp_dbl(r.c1, m);
+}
+
+DEV void fp2_mul_fp(Fp2 &r, const Fp2 &a, const Fp &s) { fp_mul(r.c0, a.c0, s); fp_mul(r.c1, a.c1, s); }
+
+// * xi = u + 1
+DEV void fp2_mul_xi(Fp2 &r, const Fp2 &a) {
+    Fp t0, t1;
+    fp_sub(t0, a.c0, a.c1);
+    fp_add(t1, a.c0, a.c1);
+    r.c0 = t0;
+    r.c1 = t1;
+}
+
+DEV void fp2_inv(Fp2 &r, const Fp2 &a) {
+    Fp n0, n1;
+    fp_sqr(n0, a.c0);
+    fp_sqr(n1, a.c1);
+    fp_add(n0, n0, n1);
+    fp_inv(n0, n0);
+    fp_mul(r.c0, a.c0, n0);
+    fp_mul(n1, a.c1, n0);
+    fp_neg(r.c1, n1);
+}
+
+DEV void fp2_frob(Fp2 &r, const Fp2 &a, int k) {
+    if (k & 1) fp2_conj(r, a);
+    else r = a;
+}
+
+DEV void fp2_const(Fp2 &r, const uint32_t (&v)[2][NL]) { fp_set(r.c0, v[0]); fp_set(r.c1, v[1]); }
+
+// ---------------------------------------------------------------- Fp6
+DEV void fp6_add(Fp6 &r, const Fp6 &a, const Fp6 &b) { fp2_add(r.c0, a.c0, b.c0); fp2_add(r.c1, a.c1, b.c1); fp2_add(r.c2, a.c2, b.c2); }
+DEV void fp6_sub(Fp6 &r, const Fp6 &a, const Fp6 &b) { fp2_sub(r.c0, a.c0, b.c0); fp2_sub(r.c1, a.c1, b.c1); fp2_sub(r.c2, a.c2, b.c2); }
+DEV void fp6_neg(Fp6 &r, const Fp6 &a) { fp2_neg(r.c0, a.c0); fp2_neg(r.c1, a.c1); fp2_neg(r.c2, a.c2); }
+DEV void fp6_dbl(Fp6 &r, const Fp6 &a) { fp2_dbl(r.c0, a.c0); fp2_dbl(r.c1, a.c1); fp2_dbl(r.c2, a.c2); }
+
+// * v: (a0, a1, a2) -> (xi a2, a0, a1)
+DEV void fp6_mul_v(Fp6 &r, const Fp6 &a) {
+    Fp2 t;
+    fp2_mul_xi(t, a.c2);
+    r.c2 = a.c1;
+    r.c1 = a.c0;
+    r.c0 = t;
+}
+
+__device__ __noinline__ void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
+    Fp2 aa, bb, cc, s, t, t1, t2, t3;
+    fp2_mul(aa, a.c0, b.c0);
+    fp2_mul(bb, a.c1, b.c1);
+    fp2_mul(cc, a.c2, b.c2);
+    fp2_add(s, a.c1, a.c2);
+    fp2_add(t, b.c1, b.c2);
+    fp2_mul(t1, s, t);
+    fp2_sub(t1, t1, bb);
+    fp2_sub(t1, t1, cc);
+    fp2_mul_xi(t1, t1);
+    fp2_add(t1, t1, aa);
+    fp2_add(s, a.c0, a.c2);
+    fp2_add(t, b.c0, b.c2);
+    fp2_mul(t3, s, t);
+    fp2_sub(t3, t3, aa);
+    fp2_add(t3, t3, bb);
+    fp2_sub(t3, t3, cc);
+    fp2_add(s, a.c0, a.c1);
+    fp2_add(t, b.c0, b.c1);
+    fp2_mul(t2, s, t);
+    fp2_sub(t2, t2, aa);
+    fp2_sub(t2, t2, bb);
+    fp2_mul_xi(cc, cc);
+    fp2_add(t2, t2, cc);
+    r.c0 = t1;
+    r.c1 = t2;
+    r.c2 = t3;
+}
+
+// (a0 + a1 v + a2 v^2)(c0 + c1 v)
+DEV void fp6_mul_by_01(Fp6 &r, const Fp6 &a, const Fp2 &c0, const Fp2 &c1) {
+    Fp2 aa, bb, s, t1, t2, t3;
+    fp2_mul(aa, a.c0, c0);
+    fp2_mul(bb, a.c1, c1);
+    fp2_add(s, a.c1, a.c2);
+    fp2_mul(t1, s, c1);
+    fp2_sub(t1, t1, bb);
+    fp2_mul_xi(t1, t1);
+    fp2_add(t1, t1, aa);
+    fp2_add(s, a.c0, a.c2);
+    fp2_mul(t3, s, c0);
+    fp2_sub(t3, t3, aa);
+    fp2_add(t3, t3, bb);
+    Fp2 cs;
+    fp2_add(cs, c0, c1);
+    fp2_add(s, a.c0, a.c1);
+    fp2_mul(t2, s, cs);
+    fp2_sub(t2, t2, aa);
+    fp2_sub(t2, t2, bb);
+    r.c0 = t1;
+    r.c1 = t2;
+    r.c2 = t3;
+}
+
+// (a0 + a1 v + a2 v^2) c1 v
+DEV void fp6_mul_by_1(Fp6 &r, const Fp6 &a, const Fp2 &c1) {
+    Fp2 t0, t1, t2;
+    fp2_mul(t2, a.c1, c1);
+    fp2_mul(t1, a.c0, c1);
+    fp2_mul(t0, a.c2, c1);
+    fp2_mul_xi(r.c0, t0);
+    r.c1 = t1;
+    r.c2 = t2;
+}
+
+DEV void fp6_inv(Fp6 &r, const Fp6 &a) {
+    Fp2 c0, c1, c2, t, u;
+    fp2_sqr(c0, a.c0);
+    fp2_mul(t, a.c1, a.c2);
+    fp2_mul_xi(t, t);
+    fp2_sub(c0, c0, t);           // a0^2 - xi a1 a2
+    fp2_sqr(c1, a.c2);
+    fp2_mul_xi(c1, c1);
+    fp2_mul(t, a.c0, a.c1);
+    fp2_sub(c1, c1, t);           // xi a2^2 - a0 a1
+    fp2_sqr(c2, a.c1);
+    fp2_mul(t, a.c0, a.c2);
+    fp2_sub(c2, c2, t);           // a1^2 - a0 a2
+    fp2_mul(t, a.c2, c1);
+    fp2_mul(u, a.c1, c2);
+    fp2_add(t, t, u);
+    fp2_mul_xi(t, t);
+    fp2_mul(u, a.c0, c0);
+    fp2_add(t, t, u);             // norm
+    fp2_inv(t, t);
+    fp2_mul(r.c0, c0, t);
+    fp2_mul(r.c1, c1, t);
+    fp2_mul(r.c2, c2, t);
+}
+
+DEV void fp6_frob(Fp6 &r, const Fp6 &a, int k) {
+    Fp2 g, t;
+    fp2_frob(r.c0, a.c0, k);
+    fp2_frob(t, a.c1, k);
+    fp2_const(g, kFrob6C1[k]);
+    fp2_mul(r.c1, t, g);
+    fp2_frob(t, a.c2, k);
+    fp2_const(g, kFrob6C2[k]);
+    fp2_mul(r.c2, t, g);
+}
+
+// ---------------------------------------------------------------- Fp12
+DEV void fp12_one(Fp12 &r) {
+    Fp2 z;
+    fp2_zero(z);
+    r.c0.c0 = z; r.c0.c1 = z; r.c0.c2 = z;
+    r.c1 = r.c0;
+    fp_set(r.c0.c0.c0, kOne);
+}
+
+DEV bool fp12_is_one(const Fp12 &a) {
+    Fp one;
+    fp_set(one, kOne);
+    return fp_eq(a.c0.c0.c0, one) && fp_is_zero(a.c0.c0.c1) && fp2_is_zero(a.c0.c1) &&
+           fp2_is_zero(a.c0.c2) && fp2_is_zero(a.c1.c0) && fp2_is_zero(a.c1.c1) &&
+           fp2_is_zero(a.c1.c2);
+}
+
+DEV void fp12_conj(Fp12 &r, const Fp12 &a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
+
+__device__ __noinline__ void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) {
+    Fp6 aa, bb, s, t;
+    fp6_mul(aa, a.c0, b.c0);
+    fp6_mul(bb, a.c1, b.c1);
+    fp6_add(s, a.c0, a.c1);
+    fp6_add(t, b.c0, b.c1);
+    fp6_mul(s, s, t);
+    fp6_sub(s, s, aa);
+    fp6_sub(r.c1, s, bb);
+    fp6_mul_v(bb, bb);
+    fp6_add(r.c0, aa, bb);
+}
+
+__device__ __noinline__ void fp12_sqr(Fp12 &r, const Fp12 &a) {
+    Fp6 ab, s, t;
+    fp6_mul(ab, a.c0, a.c1);
+    fp6_add(s, a.c0, a.c1);
+    fp6_mul_v(t, a.c1);
+    fp6_add(t, t, a.c0);
+    fp6_mul(s, s, t);
+    fp6_sub(s, s, ab);
+    fp6_mul_v(t, ab);
+    fp6_sub(r.c0, s, t);
+    fp6_dbl(r.c1, ab);
+}
+
+// f * (c0 + c1 v + c4 v w): the sparse line value
+__device__ __noinline__ void fp12_mul_by_014(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4) {
+    Fp6 aa, bb, s;
+    Fp2 o;
+    fp6_mul_by_01(aa, f.c0, c0, c1);
+    fp6_mul_by_1(bb, f.c1, c4);
+    fp2_add(o, c1, c4);
+    fp6_add(s, f.c1, f.c0);
+    fp6_mul_by_01(s, s, c0, o);
+    fp6_sub(s, s, aa);
+    fp6_sub(f.c1, s, bb);
+    fp6_mul_v(bb, bb);
+    fp6_add(f.c0, bb, aa);
+}
+
+DEV void fp12_inv(Fp12 &r, const Fp12 &a) {
+    Fp6 t0, t1;
+    fp6_mul(t0, a.c0, a.c0);
+    fp6_mul(t1, a.c1, a.c1);
+    fp6_mul_v(t1, t1);
+    fp6_sub(t0, t0, t1);          // a0^2 - v a1^2
+    fp6_inv(t0, t0);
+    fp6_mul(r.c0, a.c0, t0);
+    fp6_mul(t1, a.c1, t0);
+    fp6_neg(r.c1, t1);
+}
+
+__device__ __noinline__ void fp12_frob(Fp12 &r, const Fp12 &a, int k) {
+    Fp6 c1;
+    Fp2 g;
+    fp6_frob(r.c0, a.c0, k);
+    fp6_frob(c1, a.c1, k);
+    fp2_const(g, kFrob12C1[k]);
+    fp2_mul(r.c1.c0, c1.c0, g);
+    fp2_mul(r.c1.c1, c1.c1, g);
+    fp2_mul(r.c1.c2, c1.c2, g);
+}
+
+// f^x for the BLS parameter x < 0 (the crate's exp_by_x: pow by |x|, then
+// conjugate -- the inverse on the cyclotomic subgroup).  `shift` gives |x|>>1.
+__device__ __noinline__ void fp12_exp_by_x(Fp12 &r, const Fp12 &a, int shift) {
+    const uint64_t e = kXAbs >> shift;
+    Fp12 acc = a;
+    for (int b = 62 - shift; b >= 0; --b) {
+        fp12_sqr(acc, acc);
+        if ((e >> b) & 1u) fp12_mul(acc, acc, a);
+    }
+    fp12_conj(r, acc);
+}
+
+// ---------------------------------------------------------------- Miller loop
+struct G2Proj { Fp2 x, y, z; };
+
+// T <- 2T; line tangent at T evaluated at P = (xp, yp), scaled by 2YZ^2:
+// (3X^3 - 2Y^2 Z) + (-3X^2 Z xp) v + (2 Y Z^2 yp) v w
+DEV void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
+    Fp2 xx, w, s, ss, sss, rr, RR, B, h, t, l0, l1, l4;
+    fp2_sqr(xx, T.x);
+    fp2_dbl(w, xx);
+    fp2_add(w, w, xx);            // w = 3 X^2
+    fp2_mul(s, T.y, T.z);
+    fp2_dbl(s, s);                // s = 2 Y Z
+    fp2_sqr(ss, s);
+    fp2_mul(sss, s, ss);
+    fp2_mul(rr, T.y, s);          // R = Y s = 2 Y^2 Z
+    fp2_sqr(RR, rr);
+    fp2_add(B, T.x, rr);
+    fp2_sqr(B, B);
+    fp2_sub(B, B, xx);
+    fp2_sub(B, B, RR);            // B = (X + R)^2 - X^2 - R^2
+    fp2_mul(l0, T.x, w);
+    fp2_sub(l0, l0, rr);          // 3X^3 - 2Y^2 Z
+    fp2_mul(l1, w, T.z);
+    fp2_mul_fp(l1, l1, xp);
+    fp2_neg(l1, l1);              // -3X^2 Z xp
+    fp2_mul(l4, s, T.z);
+    fp2_mul_fp(l4, l4, yp);       // 2 Y Z^2 yp
+    fp2_sqr(h, w);
+    fp2_sub(h, h, B);
+    fp2_sub(h, h, B);             // h = w^2 - 2B
+    fp2_mul(T.x, h, s);
+    fp2_sub(t, B, h);
+    fp2_mul(t, w, t);
+    fp2_dbl(RR, RR);
+    fp2_sub(T.y, t, RR);          // w (B - h) - 2 R^2
+    T.z = sss;
+    fp12_mul_by_014(f, l0, l1, l4);
+}
+
+// T <- T + Q (Q affine); line through T and Q at P, scaled by (xq Z - X):
+// (u xq - v yq) + (-u xp) v + (v yp) v w,  u = yq Z - Y, v = xq Z - X
+DEV void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp &xp,
+                    const Fp &yp) {
+    Fp2 u, v, uu, vv, vvv, R, A, t, l0, l1, l4;
+    fp2_mul(u, yq, T.z);
+    fp2_sub(u, u, T.y);
+    fp2_mul(v, xq, T.z);
+    fp2_sub(v, v, T.x);
+    fp2_mul(l0, u, xq);
+    fp2_mul(t, v, yq);
+    fp2_sub(l0, l0, t);
+    fp2_mul_fp(l1, u, xp);
+    fp2_neg(l1, l1);
+    fp2_mul_fp(l4, v, yp);
+    fp2_sqr(uu, u);
+    fp2_sqr(vv, v);
+    fp2_mul(vvv, v, vv);
+    fp2_mul(R, vv, T.x);
+    fp2_mul(A, uu, T.z);
+    fp2_sub(A, A, vvv);
+    fp2_sub(A, A, R);
+    fp2_sub(A, A, R);             // A = uu Z - vvv - 2R
+    fp2_mul(T.x, v, A);
+    fp2_sub(t, R, A);
+    fp2_mul(t, u, t);
+    fp2_mul(vvv, vvv, T.y);
+    fp2_sub(T.y, t, vvv);
+    fp2_mul(T.z, T.z, vv);
+    fp2_mul(T.z, T.z, v);         // Z vvv
+    fp12_mul_by_014(f, l0, l1, l4);
+}
+
+// ---------------------------------------------------------------- encodings
+// 48 big-endian bytes -> limbs (little-endian words); returns false if the
+// value is not below p.  `top_mask` clears flag bits of the first byte.
+DEV bool load_be48(Fp &r, const uint8_t *src, uint32_t top_mask) {
+#pragma unroll
+    for (int w = 0; w < NL; ++w) {
+        const uint8_t *q = src + 44 - 4 * w;
+        uint32_t v = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+        r.l[w] = v;
+    }
+    r.l[NL - 1] &= top_mask;
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const uint64_t d = (uint64_t)r.l[i] - kP[i] - br;
+        br = (d >> 32) & 1u;
+    }
+    return br != 0;  // r < p
+}
+
+DEV void to_mont(Fp &r, const Fp &a) {
+    Fp r2;
+    fp_set(r2, kR2);
+    fp_mul(r, a, r2);
+}
+
+DEV void from_mont(Fp &r, const Fp &a) {
+    Fp one;
+    fp_zero(one);
+    one.l[0] = 1;
+    fp_mul(r, a, one);
+}
+
+DEV bool all_zero(const uint8_t *p, int n, uint8_t first_mask) {
+    uint32_t t = p[0] & first_mask;
+    for (int i = 1; i < n; ++i) t |= p[i];
+    return t == 0;
+}
+
+// Status of a decoded point: 0 ok, 1 infinity, 2 invalid.
+enum { PT_OK = 0, PT_INF = 1, PT_BAD = 2 };
+
+DEV int decode_g1(const uint8_t *src, Fp &x, Fp &y) {
+    const uint8_t f = src[0];
+    if (f & 0xA0) return PT_BAD;                       // compressed / sort flags
+    if (f & 0x40) return all_zero(src, 96, 0x1F) ? PT_INF : PT_BAD;
+    Fp xr, yr;
+    if (!load_be48(xr, src, 0x1FFFFFFFu) || !load_be48(yr, src + 48, 0xFFFFFFFFu)) return PT_BAD;
+    to_mont(x, xr);
+    to_mont(y, yr);
+    Fp l, r, b;
+    fp_sqr(l, y);
+    fp_sqr(r, x);
+    fp_mul(r, r, x);
+    fp_set(b, kB1);
+    fp_add(r, r, b);
+    return fp_eq(l, r) ? PT_OK : PT_BAD;               // y^2 = x^3 + 4
+}
+
+DEV int decode_g2(const uint8_t *src, Fp2 &x, Fp2 &y) {
+    const uint8_t f = src[0];
+    if (f & 0xA0) return PT_BAD;
+    if (f & 0x40) return all_zero(src, 192, 0x1F) ? PT_INF : PT_BAD;
+    Fp a, b, c, d;
+    if (!load_be48(a, src, 0x1FFFFFFFu) || !load_be48(b, src + 48, 0xFFFFFFFFu) ||
+        !load_be48(c, src + 96, 0xFFFFFFFFu) || !load_be48(d, src + 144, 0xFFFFFFFFu))
+        return PT_BAD;
+    to_mont(x.c1, a);
+    to_mont(x.c0, b);
+    to_mont(y.c1, c);
+    to_mont(y.c0, d);
+    Fp2 l, r, bb;
+    fp2_sqr(l, y);
+    fp2_sqr(r, x);
+    fp2_mul(r, r, x);
+    fp_set(bb.c0, kB1);
+    bb.c1 = bb.c0;                                     // 4 (u + 1)
+    fp2_add(r, r, bb);
+    return fp2_eq(l, r) ? PT_OK : PT_BAD;
+}
+
+// Limb-major workspace: word w of pairing i at ws[w * n + i].
+DEV void store_f12(uint32_t *ws, size_t n, size_t i, const Fp12 &f) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&f);
+#pragma unroll 4
+    for (int w = 0; w < 12 * NL; ++w) ws[(size_t)w * n + i] = src[w];
+}
+
+DEV void load_f12(Fp12 &f, const uint32_t *ws, size_t n, size_t i) {
+    uint32_t *dst = reinterpret_cast<uint32_t *>(&f);
+#pragma unroll 4
+    for (int w = 0; w < 12 * NL; ++w) dst[w] = ws[(size_t)w * n + i];
+}
+
+constexpr int kPairBlock = 64;
+
+// Kernel 1: one Miller loop per lane.  Pairing i takes G1 point g1[i] and G2
+// point g2[i]; with `negate_odd`, odd pairings negate their G1 point (the
+// c of a check a,b == c,d sits at pairing 2i+1).  status[i] gets the point
+// status (max of the two); an infinity or invalid input leaves f = 1.
+__global__ __launch_bounds__(kPairBlock) void miller_kernel(
+    const uint8_t *__restrict__ g1, size_t g1_stride, const uint8_t *__restrict__ g2,
+    size_t g2_stride, size_t n, int pair_inputs, uint32_t *__restrict__ ws,
+    uint8_t *__restrict__ status) {
+    const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    if (i >= n) return;
+    // pair_inputs: pairing 2c reads (a_c, b_c) from the first halves of the
+    // arrays, 2c+1 reads (c_c, d_c) from the second halves (see launcher)
+    const uint8_t *p1 = g1 + i * g1_stride;
+    const uint8_t *p2 = g2 + i * g2_stride;
+    Fp xp, yp;
+    Fp2 xq, yq;
+    const int s1 = decode_g1(p1, xp, yp);
+    const int s2 = decode_g2(p2, xq, yq);
+    Fp12 f;
+    fp12_one(f);
+    const int st = s1 > s2 ? s1 : s2;
+    if (st == PT_OK && s1 == PT_OK && s2 == PT_OK) {
+        if (pair_inputs && (i & 1)) fp_neg(yp, yp);
+        G2Proj T;
+        T.x = xq;
+        T.y = yq;
+        fp_set(T.z.c0, kOne);
+        fp_zero(T.z.c1);
+        for (int b = 62; b >= 0; --b) {
+            fp12_sqr(f, f);
+            miller_dbl(T, f, xp, yp);
+            if ((kXAbs >> b) & 1u) miller_add(T, f, xq, yq, xp, yp);
+        }
+        fp12_conj(f, f);
+    }
+    status[i] = (uint8_t)((s1 == PT_BAD || s2 == PT_BAD) ? PT_BAD : PT_OK);
+    store_f12(ws, n, i, f);
+}
+
+// The crate's final exponentiation (Bls12::final_exponentiation): easy part
+// f^((p^6 - 1)(p^2 + 1)), then the hard-part chain.
+DEV void final_exp(Fp12 &out, const Fp12 &f) {
+    Fp12 r, t, y0, y1, y2, y3;
+    fp12_inv(t, f);
+    fp12_conj(r, f);
+    fp12_mul(r, r, t);            // f^(p^6 - 1)
+    fp12_frob(t, r, 2);
+    fp12_mul(r, t, r);            // ^(p^2 + 1)
+    fp12_sqr(y0, r);
+    fp12_exp_by_x(y1, y0, 0);
+    fp12_exp_by_x(y2, y1, 1);
+    fp12_conj(y3, r);
+    fp12_mul(y1, y1, y3);
+    fp12_conj(y1, y1);
+    fp12_mul(y1, y1, y2);
+    fp12_exp_by_x(y2, y1, 0);
+    fp12_exp_by_x(y3, y2, 0);
+    fp12_conj(y1, y1);
+    fp12_mul(y3, y3, y1);
+    fp12_conj(y1, y1);
+    fp12_frob(y1, y1, 3);
+    fp12_frob(y2, y2, 2);
+    fp12_mul(y1, y1, y2);
+    fp12_exp_by_x(y2, y3, 0);
+    fp12_mul(y2, y2, y0);
+    fp12_mul(y2, y2, r);
+    fp12_mul(y1, y1, y2);
+    fp12_frob(y2, y3, 1);
+    fp12_mul(out, y1, y2);
+}
+
+DEV void store_be48(uint8_t *dst, const Fp &a) {
+    Fp c;
+    from_mont(c, a);
+#pragma unroll
+    for (int w = 0; w < NL; ++w) {
+        const uint32_t v = c.l[NL - 1 - w];
+        dst[4 * w + 0] = (uint8_t)(v >> 24);
+        dst[4 * w + 1] = (uint8_t)(v >> 16);
+        dst[4 * w + 2] = (uint8_t)(v >> 8);
+        dst[4 * w + 3] = (uint8_t)v;
+    }
+}
+
+// Kernel 2: one final exponentiation per lane.  `per_out` Miller values
+// (1: a pairing, 2: a check) are multiplied first.  gt_out (if set) gets the
+// 576-byte GT value; ok_out (if set) gets 1 if the value is 1 (the check
+// holds), 0 if not, 2 if an input point was invalid.
+__global__ __launch_bounds__(kPairBlock) void final_exp_kernel(
+    const uint32_t *__restrict__ ws, size_t n_miller, size_t n_out, int per_out,
+    const uint8_t *__restrict__ status, uint8_t *__restrict__ gt_out,
+    uint8_t *__restrict__ ok_out) {
+    const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    if (i >= n_out) return;
+    Fp12 f;
+    load_f12(f, ws, n_miller, i * per_out);
+    int bad = status[i * per_out] == PT_BAD;
+    for (int j = 1; j < per_out; ++j) {
+        Fp12 g;
+        load_f12(g, ws, n_miller, i * per_out + j);
+        fp12_mul(f, f, g);
+        bad |= status[i * per_out + j] == PT_BAD;
+    }
+    Fp12 e;
+    final_exp(e, f);
+    if (gt_out) {
+        uint8_t *dst = gt_out + i * 576;
+        const Fp2 *c = &e.c0.c0;
+        const Fp2 *cs[6] = {&e.c0.c0, &e.c0.c1, &e.c0.c2, &e.c1.c0, &e.c1.c1, &e.c1.c2};
+        (void)c;
+        for (int k = 0; k < 6; ++k) {
+            store_be48(dst + 96 * k, cs[k]->c0);
+            store_be48(dst + 96 * k + 48, cs[k]->c1);
+        }
+    }
+    if (ok_out) ok_out[i] = bad ? 2 : (fp12_is_one(e) ? 1 : 0);
+}
+
+}  // namespace
+
+hipError_t launch_pairing_miller(const uint8_t *g1, size_t g1_stride, const uint8_t *g2,
+                                 size_t g2_stride, size_t n, int pair_inputs, uint32_t *ws,
+                                 uint8_t *status, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((n + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(miller_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, g1_stride, g2,
+                       g2_stride, n, pair_inputs, ws, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_out, int per_out,
+                                const uint8_t *status, uint8_t *gt_out, uint8_t *ok_out,
+                                hipStream_t s) {
+    if (n_out == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((n_out + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(final_exp_kernel, dim3(blocks), dim3(kPairBlock), 0, s, ws, n_miller,
+                       n_out, per_out, status, gt_out, ok_out);
+    return hipGetLastError();
+}
+
+}  // namespace hbrbc

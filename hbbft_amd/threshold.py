@@ -1,0 +1,137 @@
+"""Threshold-decrypt share verification on the MI355X.
+
+hbbft's `ThresholdDecrypt` (/root/reference/src/threshold_decrypt.rs) checks
+every ciphertext once (`ct.verify()`, line 142) and every received decryption
+share (`pk.verify_decryption_share(share, ct)`, lines 220-228), both from
+`threshold_crypto` (rev 624eeee):
+
+    Ciphertext::verify                      e(G1::one(), W) == e(U, H)
+    PublicKeyShare::verify_decryption_share e(share, H)     == e(pk_i, W)
+
+with H = hash_g1_g2(U, V), a G2 point the caller computes once per
+ciphertext (SHA3-256 and a ChaCha-seeded G2 sample -- host work, not on the
+bulk path).  In an epoch every node verifies N shares of each of N
+ciphertexts, so the pairing checks come in batches of N^2 per node; this
+module runs them through `hbrbc_pairing_check_batch` (hbbft_amd/csrc/
+pairing.hip): one Miller loop per lane, one final exponentiation per check.
+
+Points are the crate's uncompressed encodings (G1: 96 bytes, G2: 192 bytes,
+big-endian; see include/hbrbc.h).  There is no CPU fallback: without the
+library or a GPU the calls raise `HbrbcUnavailable`.
+"""
+import ctypes
+
+from . import HbrbcUnavailable, RseError, _check, lib  # noqa: F401
+
+G1_BYTES = 96
+G2_BYTES = 192
+GT_BYTES = 576
+
+# G1::one() (the standard generator), uncompressed: the `a` of Ciphertext::verify.
+G1_ONE = bytes.fromhex(
+    "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
+    "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
+
+CHECK_OK, CHECK_FAIL, CHECK_INVALID = 1, 0, 2
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def workspace(pairings, device=0):
+    """Device workspace for `pairings` Miller loops (reusable across calls)."""
+    torch = _torch()
+    n = lib().hbrbc_pairing_workspace_size(pairings)
+    return torch.empty(max(n, 1), dtype=torch.uint8, device="cuda:%d" % device)
+
+
+def _stream(dev, stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def pairing_batch(g1, g2, ws=None, stream=None):
+    """`PEngine::pairing(g1[i], g2[i])` for every row: g1 uint8 [n, 96], g2 uint8
+    [n, 192] on one device.  Returns (gt uint8 [n, 576], status uint8 [n];
+    0 ok, 2 invalid point)."""
+    torch = _torch()
+    n = g1.shape[0]
+    assert g1.shape == (n, G1_BYTES) and g2.shape == (n, G2_BYTES), (g1.shape, g2.shape)
+    assert g1.is_contiguous() and g2.is_contiguous() and g1.device == g2.device
+    gt = torch.empty((n, GT_BYTES), dtype=torch.uint8, device=g1.device)
+    st = torch.empty((n,), dtype=torch.uint8, device=g1.device)
+    if ws is None:
+        ws = workspace(n, g1.device.index)
+    assert ws.numel() >= lib().hbrbc_pairing_workspace_size(n)
+    _check(lib().hbrbc_pairing_batch(g1.data_ptr(), g2.data_ptr(), n, gt.data_ptr(),
+                                     st.data_ptr(), ws.data_ptr(), _stream(g1.device, stream)))
+    return gt, st
+
+
+def pairing_check_batch(g1, g2, ws=None, stream=None):
+    """count checks e(a_i, b_i) == e(c_i, d_i): g1 uint8 [2 count, 96] = a_0,
+    c_0, a_1, c_1, ...; g2 uint8 [2 count, 192] = b_0, d_0, ....  Returns
+    uint8 [count]: 1 equal, 0 not, 2 invalid point."""
+    torch = _torch()
+    n2 = g1.shape[0]
+    assert n2 % 2 == 0 and g1.shape == (n2, G1_BYTES) and g2.shape == (n2, G2_BYTES)
+    assert g1.is_contiguous() and g2.is_contiguous() and g1.device == g2.device
+    ok = torch.empty((n2 // 2,), dtype=torch.uint8, device=g1.device)
+    if ws is None:
+        ws = workspace(n2, g1.device.index)
+    assert ws.numel() >= lib().hbrbc_pairing_workspace_size(n2)
+    _check(lib().hbrbc_pairing_check_batch(g1.data_ptr(), g2.data_ptr(), n2 // 2, ok.data_ptr(),
+                                           ws.data_ptr(), _stream(g1.device, stream)))
+    return ok
+
+
+def pairing_check(a, b, c, d):
+    """Per-call shim: e(a, b) == e(c, d) for host byte strings (one device
+    round trip).  Raises RseError(InvalidArgument) on an invalid point."""
+    for x, n in ((a, G1_BYTES), (b, G2_BYTES), (c, G1_BYTES), (d, G2_BYTES)):
+        if len(x) != n:
+            raise ValueError("point encoding of %d bytes, expected %d" % (len(x), n))
+    res = ctypes.c_int(0)
+    _check(lib().hbrbc_pairing_check(bytes(a), bytes(b), bytes(c), bytes(d), ctypes.byref(res)))
+    return bool(res.value)
+
+
+def _pack(items, device):
+    """[(a, b, c, d)] host bytes -> (g1 [2n, 96], g2 [2n, 192]) on `device`."""
+    import numpy as np
+    torch = _torch()
+    n = len(items)
+    g1 = np.empty((2 * n, G1_BYTES), dtype=np.uint8)
+    g2 = np.empty((2 * n, G2_BYTES), dtype=np.uint8)
+    for i, (a, b, c, d) in enumerate(items):
+        g1[2 * i] = np.frombuffer(a, np.uint8)
+        g1[2 * i + 1] = np.frombuffer(c, np.uint8)
+        g2[2 * i] = np.frombuffer(b, np.uint8)
+        g2[2 * i + 1] = np.frombuffer(d, np.uint8)
+    dev = "cuda:%d" % device
+    return torch.from_numpy(g1).to(dev), torch.from_numpy(g2).to(dev)
+
+
+def verify_decryption_shares(items, device=0):
+    """Batched `PublicKeyShare::verify_decryption_share` (threshold_decrypt.rs:
+    220-228): items = [(share G1, pk_share G1, hash G2, W G2)] host bytes.
+    Returns a list of bools (an invalid point is False, as a share that does
+    not deserialise never reaches the check)."""
+    if not items:
+        return []
+    g1, g2 = _pack([(s, h, pk, w) for s, pk, h, w in items], device)
+    ok = pairing_check_batch(g1, g2).cpu().tolist()
+    return [v == CHECK_OK for v in ok]
+
+
+def verify_ciphertexts(items, device=0):
+    """Batched `Ciphertext::verify` (threshold_decrypt.rs:142): items =
+    [(U G1, W G2, hash G2)]; e(G1::one(), W) == e(U, hash)."""
+    if not items:
+        return []
+    g1, g2 = _pack([(G1_ONE, w, u, h) for u, w, h in items], device)
+    ok = pairing_check_batch(g1, g2).cpu().tolist()
+    return [v == CHECK_OK for v in ok]

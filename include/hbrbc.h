@@ -382,6 +382,46 @@ int hbrbc_profile_reset(hbrbc_ctx *ctx);
 int hbrbc_profile_read(hbrbc_ctx *ctx, double *ms_out, uint64_t *launches_out);
 const char *hbrbc_stage_name(int stage);
 
+/* ---- threshold-decrypt share verification --------------- */
+/* BLS12-381 pairings of the `pairing` crate as `threshold_crypto` (rev 624eeee,
+ * Cargo.toml:36) uses them behind hbbft's ThresholdDecrypt:
+ *   `Ciphertext::verify`                  (threshold_decrypt.rs:142)
+ *       e(G1::one(), W) == e(U, hash_g1_g2(U, V))
+ *   `PublicKeyShare::verify_decryption_share` (threshold_decrypt.rs:220-228)
+ *       e(share, hash_g1_g2(U, V)) == e(pk_i, W)
+ * Points use the crate's uncompressed encodings: G1 = 96 bytes x || y, G2 =
+ * 192 bytes x.c1 || x.c0 || y.c1 || y.c0, big-endian, infinity = flag 0x40 in
+ * byte 0 with every other bit zero.  Non-canonical coordinates (>= p), set
+ * compression/sort flags and points off the curve are rejected per item;
+ * subgroup membership is assumed (the crate's deserialisation checks it).
+ * hash_g1_g2 (SHA3 + ChaCha-seeded G2 sampling, once per ciphertext) stays
+ * with the caller, which passes the G2 point. */
+#define HBRBC_G1_BYTES 96
+#define HBRBC_G2_BYTES 192
+#define HBRBC_GT_BYTES 576
+/* Device workspace bytes for `pairings` Miller loops. */
+size_t hbrbc_pairing_workspace_size(size_t pairings);
+/* `PEngine::pairing(g1[i], g2[i])` for i < count: gt_out + 576 i receives the
+ * GT value (the crate's Fq12 after its final exponentiation, tower order
+ * c0.c0.c0, c0.c0.c1, c0.c1.c0, ..., c1.c2.c1, each coefficient 48 bytes
+ * big-endian); status_out[i] = 0 ok, 2 invalid point (the value is then 1).
+ * An infinity on either side gives 1.  Device memory, async on `stream`. */
+int hbrbc_pairing_batch(const uint8_t *g1, const uint8_t *g2, size_t count, uint8_t *gt_out,
+                        uint8_t *status_out, void *workspace, void *stream);
+/* count checks e(a_i, b_i) == e(c_i, d_i): g1 holds a_0, c_0, a_1, c_1, ...
+ * (2 count points), g2 holds b_0, d_0, b_1, d_1, ....  ok_out[i] = 1 if
+ * equal, 0 if not, 2 if any of the four points is invalid.  For
+ * verify_decryption_share: a = share, b = hash, c = pk_i, d = W; for
+ * Ciphertext::verify: a = G1::one(), b = W, c = U, d = hash.
+ * workspace >= hbrbc_pairing_workspace_size(2 count).  Device memory, async. */
+int hbrbc_pairing_check_batch(const uint8_t *g1, const uint8_t *g2, size_t count,
+                              uint8_t *ok_out, void *workspace, void *stream);
+/* Per-call shim on host memory (one check, synchronous, current device):
+ * *result = 1 if e(a, b) == e(c, d), 0 if not; HBRBC_E_INVALID_ARG for an
+ * invalid point. */
+int hbrbc_pairing_check(const uint8_t a[96], const uint8_t b[192], const uint8_t c[96],
+                        const uint8_t d[192], int *result);
+
 #ifdef __cplusplus
 }
 #endif

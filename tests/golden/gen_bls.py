@@ -1,0 +1,49 @@
+"""Writes tests/golden/bls_vectors.json: BLS12-381 pairing vectors from the
+CPU restatement (oracle/bls_oracle.py) for the f4 parity tests.
+
+Run from the repo root: python tests/golden/gen_bls.py.  Each vector holds
+the uncompressed point encodings and the GT bytes (576, tower order) of
+the `pairing` crate's e(P, Q) = f^(3 (p^12-1)/r) (see the oracle header for
+what pins that); `checks` hold threshold-decrypt shaped checks with their
+expected outcomes.  Scalars are fixed, so the file is reproducible.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import bls_oracle as B  # noqa: E402
+
+SCALARS_1 = [1, 2, 3, 0x1234567, B.R - 1, 0x5eed_1e55_0f_c0ffee]
+SCALARS_2 = [1, 5, 0xabcdef, B.R - 2]
+
+
+def main():
+    pairs = [(1, 1), (2, 1), (1, 2), (3, 5), (0x1234567, 0xabcdef), (B.R - 1, 1),
+             (0x5eed_1e55_0f_c0ffee, B.R - 2)]
+    vectors = []
+    for a, b in pairs:
+        p1 = B.g1_mul(B.G1_GEN, a)
+        q2 = B.g2_mul(B.G2_GEN, b)
+        gt = B.pairing(p1, q2)
+        vectors.append({"g1_scalar": a, "g2_scalar": b, "g1": B.g1_bytes(p1).hex(),
+                        "g2": B.g2_bytes(q2).hex(), "gt": B.gt_bytes(gt).hex()})
+    checks = []
+    for sk, r_enc, h, tamper in [(7, 11, 13, False), (7, 11, 13, True),
+                                 (0xdead_beef, 0x1234_5678_9abc, 0x42, False),
+                                 (B.R - 3, 99, 0x77, True)]:
+        share, H, pk, W = B.decryption_share_case(sk, r_enc, h, tamper)
+        checks.append({"a": B.g1_bytes(share).hex(), "b": B.g2_bytes(H).hex(),
+                       "c": B.g1_bytes(pk).hex(), "d": B.g2_bytes(W).hex(),
+                       "expect": not tamper, "kind": "verify_decryption_share"})
+    out = {"source": "oracle/bls_oracle.py (restatement of the pairing crate's BLS12-381)",
+           "pairings": vectors, "checks": checks}
+    path = os.path.join(ROOT, "tests", "golden", "bls_vectors.json")
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote", path, len(vectors), "pairings", len(checks), "checks")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,69 @@
+"""CPU checks of the BLS12-381 restatement (oracle/bls_oracle.py) that the
+f4 GPU parity tests compare against: generator coordinates,
+field and Frobenius identities, the final-exponentiation chain against its
+specification, bilinearity, and the committed golden vectors."""
+import json
+import os
+import random
+
+import pytest
+
+from oracle import bls_oracle as B
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))
+
+
+def test_generators_on_curve_and_in_r_torsion():
+    assert B.g1_on_curve(B.G1_GEN) and B.g2_on_curve(B.G2_GEN)
+    assert B.g1_mul(B.G1_GEN, B.R) is None
+    assert B.g2_mul(B.G2_GEN, B.R) is None
+    assert B.P % 6 == 1 and B.P % 4 == 3      # sextic twist, u^2 = -1 non-residue
+
+
+def test_fp12_identities():
+    rng = random.Random(1)
+    a = [rng.randrange(B.P) for _ in range(12)]
+    assert B.f12mul(a, B.f12inv(a)) == B.F12_ONE
+    assert B.f12frob(a, 1) == B.f12pow(a, B.P)
+    assert B.f12frob(a, 6) == B.f12conj(a)
+    assert B.from_tower(B.to_tower(a)) == a
+
+
+def test_final_exponentiation_chain_is_cube_of_reduced_pairing():
+    """The crate's hard-part chain evaluates f^(3 (p^12-1)/r)."""
+    rng = random.Random(2)
+    f = [rng.randrange(B.P) for _ in range(12)]
+    assert B.final_exponentiation(f) == B.final_exponentiation_plain(f, 3)
+    assert B.final_exponentiation(f) != B.final_exponentiation_plain(f, 1)
+
+
+def test_bilinear_nondegenerate_order_r():
+    e = B.pairing(B.G1_GEN, B.G2_GEN)
+    assert e != B.F12_ONE
+    assert B.f12pow(e, B.R) == B.F12_ONE
+    e6 = B.pairing(B.g1_mul(B.G1_GEN, 2), B.g2_mul(B.G2_GEN, 3))
+    assert e6 == B.f12pow(e, 6)
+    assert B.pairing(None, B.G2_GEN) == B.F12_ONE
+    assert B.pairing(B.g1_neg(B.G1_GEN), B.G2_GEN) == B.f12inv(e)
+
+
+def test_decryption_share_shapes():
+    share, H, pk, W = B.decryption_share_case(5, 9, 3)
+    assert B.pairing_check(share, H, pk, W)
+    share, H, pk, W = B.decryption_share_case(5, 9, 3, tamper=True)
+    assert not B.pairing_check(share, H, pk, W)
+
+
+@pytest.mark.parametrize("idx", [0, 3])
+def test_oracle_reproduces_golden(idx):
+    v = GOLD["pairings"][idx]
+    p1 = B.g1_mul(B.G1_GEN, v["g1_scalar"])
+    q2 = B.g2_mul(B.G2_GEN, v["g2_scalar"])
+    assert B.g1_bytes(p1).hex() == v["g1"] and B.g2_bytes(q2).hex() == v["g2"]
+    assert B.gt_bytes(B.pairing(p1, q2)).hex() == v["gt"]
+
+
+def test_golden_g1_encoding_of_generator_matches_product_constant():
+    from hbbft_amd import threshold
+    assert threshold.G1_ONE == B.g1_bytes(B.G1_GEN)

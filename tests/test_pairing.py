@@ -1,0 +1,111 @@
+"""GPU parity of the f4 path (threshold-decrypt share verification,
+hbbft_amd/csrc/pairing.hip) against the BLS12-381 restatement
+(oracle/bls_oracle.py) and its golden vectors: GT values bit-exact, check
+outcomes exact, invalid encodings rejected per item."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import bls_oracle as B
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(rows, width):
+    import torch
+    a = np.frombuffer(b"".join(rows), np.uint8).reshape(len(rows), width)
+    return torch.from_numpy(a.copy()).to("cuda:0")
+
+
+def test_pairing_batch_matches_golden():
+    from hbbft_amd import threshold as T
+    vs = GOLD["pairings"]
+    g1 = _t([bytes.fromhex(v["g1"]) for v in vs], 96)
+    g2 = _t([bytes.fromhex(v["g2"]) for v in vs], 192)
+    gt, st = T.pairing_batch(g1, g2)
+    assert st.cpu().tolist() == [0] * len(vs)
+    for i, v in enumerate(vs):
+        assert bytes(gt[i].cpu().numpy()).hex() == v["gt"], i
+
+
+def test_pairing_batch_infinity_and_invalid():
+    from hbbft_amd import threshold as T
+    one = B.gt_bytes(B.F12_ONE)
+    e = B.gt_bytes(B.pairing(B.G1_GEN, B.G2_GEN))
+    g1_ok, g2_ok = B.g1_bytes(B.G1_GEN), B.g2_bytes(B.G2_GEN)
+    off_curve = bytearray(g1_ok)
+    off_curve[-1] ^= 1
+    big = bytes.fromhex("%096x" % B.P) + g1_ok[48:]          # x = p: not canonical
+    compressed = bytes([g1_ok[0] | 0x80]) + g1_ok[1:]
+    inf_dirty = b"\x40" + b"\0" * 94 + b"\x01"
+    cases = [(g1_ok, g2_ok, e, 0), (B.g1_bytes(None), g2_ok, one, 0),
+             (g1_ok, B.g2_bytes(None), one, 0), (bytes(off_curve), g2_ok, one, 2),
+             (big, g2_ok, one, 2), (compressed, g2_ok, one, 2), (inf_dirty, g2_ok, one, 2)]
+    g1 = _t([c[0] for c in cases], 96)
+    g2 = _t([c[1] for c in cases], 192)
+    gt, st = T.pairing_batch(g1, g2)
+    assert st.cpu().tolist() == [c[3] for c in cases]
+    for i, c in enumerate(cases):
+        assert bytes(gt[i].cpu().numpy()) == c[2], i
+
+
+def test_check_batch_golden_and_mixed():
+    from hbbft_amd import threshold as T
+    cs = GOLD["checks"]
+    items = [(bytes.fromhex(c["a"]), bytes.fromhex(c["c"]), bytes.fromhex(c["b"]),
+              bytes.fromhex(c["d"])) for c in cs]
+    assert T.verify_decryption_shares(items) == [c["expect"] for c in cs]
+    for c in cs:
+        assert T.pairing_check(*(bytes.fromhex(c[k]) for k in "abcd")) == c["expect"]
+
+
+def test_ciphertext_verify_shape():
+    from hbbft_amd import threshold as T
+    r_enc, h = 0x1234, 0x99
+    H = B.g2_mul(B.G2_GEN, h)
+    U = B.g1_mul(B.G1_GEN, r_enc)
+    W = B.g2_mul(H, r_enc)
+    W_bad = B.g2_mul(H, r_enc + 1)
+    got = T.verify_ciphertexts([(B.g1_bytes(U), B.g2_bytes(W), B.g2_bytes(H)),
+                                (B.g1_bytes(U), B.g2_bytes(W_bad), B.g2_bytes(H))])
+    assert got == [True, False]
+
+
+def test_check_batch_bilinearity_at_size():
+    """4096 checks e(a P_i, b Q_j) == e(b P_i, a Q_j) (true) and with b+1 on one
+    side (false), from small pools of oracle-built points; exact outcomes."""
+    from hbbft_amd import threshold as T
+    rng = random.Random(7)
+    sa = [rng.randrange(1, B.R) for _ in range(4)]
+    sb = [rng.randrange(1, B.R) for _ in range(4)]
+    P = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+    Q = B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))
+    g1p = {s: B.g1_bytes(B.g1_mul(P, s)) for s in sa + sb + [x + 1 for x in sb]}
+    g2p = {s: B.g2_bytes(B.g2_mul(Q, s)) for s in sa + sb}
+    items, expect = [], []
+    for i in range(4096):
+        a, b = sa[i % 4], sb[(i // 4) % 4]
+        good = (i // 16) % 3 != 0
+        c_s = b if good else b + 1
+        items.append((g1p[a], g2p[b], g1p[c_s], g2p[a]))
+        expect.append(good)
+    g1 = _t([x for it in items for x in (it[0], it[2])], 96)
+    g2 = _t([x for it in items for x in (it[1], it[3])], 192)
+    ok = T.pairing_check_batch(g1, g2).cpu().tolist()
+    assert ok == [1 if e else 0 for e in expect]
+
+
+def test_per_call_rejects_invalid_point():
+    from hbbft_amd import RseError
+    from hbbft_amd import threshold as T
+    bad = bytearray(B.g1_bytes(B.G1_GEN))
+    bad[-1] ^= 1
+    with pytest.raises(RseError):
+        T.pairing_check(bytes(bad), B.g2_bytes(B.G2_GEN), B.g1_bytes(B.G1_GEN),
+                        B.g2_bytes(B.G2_GEN))
