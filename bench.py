@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="target seconds per CPU rep")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--f4-checks", type=int, default=F4_CHECKS,
+                    help="f4 leg: pairing checks per GPU per step (0 = skip the leg)")
+    ap.add_argument("--f4-steps", type=int, default=3)
     ap.add_argument("--streams", type=int, default=1,
                     help="instance mode: sub-batches per step, each on its own HIP stream")
     ap.add_argument("--vsubs", type=int, default=4,
@@ -544,6 +547,132 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
 
 
 # --------------------------------------------------------------------- main --
+# ------------------------------------------------ f4: threshold-decrypt checks --
+F4_CHECKS = 131072     # 32 epochs x 64 ciphertexts x 64 decryption shares (N=64)
+F4_METRIC = "threshold-decrypt share verifications/s (BLS12-381 pairing checks)"
+
+
+def pairing_ops_per_check():
+    """32-bit lane-ops per check (2 Miller loops + 1 final exponentiation):
+    SQ_INSTS_VALU x 64 / checks from the committed counter pass, or None."""
+    p = os.path.join(ROOT, "profiles", "pairing_valu_ops.json")
+    try:
+        d = json.load(open(p))
+        return float(d["ops_per_check"]), d["source"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+
+
+def f4_cpu_check(item):
+    from oracle import bls_oracle as B
+    a, b, c, d = (bytes.fromhex(item[k]) for k in "abcd")
+
+    def g1(x):
+        return None if x[0] & 0x40 else (int.from_bytes(x[:48], "big"), int.from_bytes(x[48:], "big"))
+
+    def g2(x):
+        if x[0] & 0x40:
+            return None
+        v = [int.from_bytes(x[i:i + 48], "big") for i in range(0, 192, 48)]
+        return ((v[1], v[0]), (v[3], v[2]))
+    return B.pairing_check(g1(a), g2(b), g1(c), g2(d)) == item["expect"]
+
+
+def f4_cpu_baseline(pool, reps):
+    """oracle/bls_oracle.py (pure-Python restatement of the pairing crate) on the
+    cgroup's cores (spawned worker processes) and on one core; median of reps."""
+    import multiprocessing as mp
+    cpus = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
+    procs = max(1, min(cpus, int(quota)) if quota else cpus)
+    items = [pool[i % len(pool)] for i in range(2 * procs)]
+    times = []
+    with mp.get_context("spawn").Pool(procs) as p:
+        p.map(f4_cpu_check, items[:procs])                      # warm-up / import
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ok = p.map(f4_cpu_check, items)
+            times.append(time.perf_counter() - t0)
+            assert all(ok), "CPU restatement disagrees with the fixture outcomes"
+    times.sort()
+    t1 = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        assert f4_cpu_check(pool[0])
+        t1.append(time.perf_counter() - t0)
+    t1.sort()
+    med, med1 = times[len(times) // 2], t1[len(t1) // 2]
+    return {"value": len(items) / med, "unit": "checks/s", "cores": procs, "kind": "port",
+            "reps": reps, "single_core": {"value": 1.0 / med1, "unit": "checks/s", "cores": 1},
+            "sample": "%d checks (the fixture pool) through oracle/bls_oracle.py, a pure-Python "
+                      "big-integer restatement of the pairing crate (far slower than the Rust "
+                      "crate, which cannot be built here), %d worker processes; median of %d "
+                      "reps %.2f s" % (len(items), procs, reps, med)}
+
+
+def run_threshold(args, rank, world, dev):
+    """f4 leg: F4_CHECKS verify_decryption_share checks per GPU per step, e(share,
+    H) == e(pk_i, W), through hbrbc_pairing_check_batch; inputs tile the 32
+    committed fixture checks (tests/golden/bls_vectors.json, one in four
+    tampered), outcomes checked exactly after warm-up."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from hbbft_amd import threshold as T
+    pool = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))["bench_pool"]
+    n = args.f4_checks
+    g1 = np.empty((2 * n, 96), np.uint8)
+    g2 = np.empty((2 * n, 192), np.uint8)
+    enc = [[np.frombuffer(bytes.fromhex(c[k]), np.uint8) for k in "abcd"] for c in pool]
+    idx = (np.arange(n) + rank) % len(pool)
+    for j, e in enumerate(enc):
+        sel = np.nonzero(idx == j)[0]
+        g1[2 * sel], g2[2 * sel], g1[2 * sel + 1], g2[2 * sel + 1] = e[0], e[1], e[2], e[3]
+    expect = torch.tensor([1 if pool[j]["expect"] else 0 for j in idx], dtype=torch.uint8)
+    d1, d2 = torch.from_numpy(g1).to(dev), torch.from_numpy(g2).to(dev)
+    ws = T.workspace(2 * n, dev.index)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(max(1, args.warmup)):
+        ok = T.pairing_check_batch(d1, d2, ws)
+    torch.cuda.synchronize(dev)
+    if not torch.equal(ok.cpu(), expect):
+        raise SystemExit("bench f4: check outcomes differ from the fixtures")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.f4_steps):
+        T.pairing_check_batch(d1, d2, ws)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = max_over_ranks(time.perf_counter() - t0, world, dev)
+    ev_ms = e0.elapsed_time(e1)
+    checks = world * n * args.f4_steps
+    ops, src = pairing_ops_per_check()
+    roof = None
+    if ops is not None:
+        rate = n * args.f4_steps / (ev_ms / 1e3) * ops
+        roof = {"bound": "valu", "achieved": rate / 1e12, "peak": VALU_PEAK_OPS / 1e12,
+                "unit": "T lane-ops/s", "frac": rate / VALU_PEAK_OPS, "traffic": None,
+                "ops_per_check": ops, "ops_per_check_source": src,
+                "note": "miller_kernel + final_exp_kernel together, timed with HIP events on "
+                        "the launch stream; the mix is ~20% v_mad_u64_u32 (multi-pass)"}
+    return {"metric": F4_METRIC, "value": checks / wall, "unit": "checks/s",
+            "ms_per_step": wall / args.f4_steps * 1e3, "steps": args.f4_steps,
+            "device_ms_per_step": ev_ms / args.f4_steps, "pairings_per_step": 2 * n,
+            "scaling": "weak", "dtype": "u32 (12-limb Montgomery Fp)",
+            "config": {"workload": "f4: verify_decryption_share e(share, H) == e(pk_i, W), "
+                                   "%d checks per GPU per step (32 epochs x 64 ciphertexts x 64 "
+                                   "shares, N=64)" % n, "checks_per_gpu": n},
+            "data": "the 32 fixture checks of tests/golden/bls_vectors.json tiled "
+                    "(one in four tampered); outcomes verified exactly",
+            "roofline": roof}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -590,6 +719,21 @@ def main():
                 vobj = {"error": "%s: %s" % (type(e).__name__, e)}
                 print("bench: validator-sharded run failed: %r" % (e,), file=sys.stderr)
 
+    f4 = None
+    if args.f4_checks > 0:
+        torch.cuda.empty_cache()
+        try:
+            f4 = run_threshold(args, rank, world, dev)
+        except SystemExit:
+            raise
+        except Exception as e:  # noqa: BLE001  (secondary leg: keep the headline line)
+            f4 = {"error": "%s: %s" % (type(e).__name__, e)}
+            print("bench: f4 leg failed: %r" % (e,), file=sys.stderr)
+        if rank == 0 and world == 1 and not args.no_cpu and "error" not in f4:
+            pool = json.load(open(os.path.join(ROOT, "tests", "golden",
+                                               "bls_vectors.json")))["bench_pool"]
+            f4["cpu_baseline"] = f4_cpu_baseline(pool, 3)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         f = (n - 1) // 3
@@ -611,6 +755,8 @@ def main():
                     vobj["cpu_baseline"] = dict(cpu, note="the same per-instance pipeline; the "
                                                 "CPU leg decodes each instance once")
                 line["validators"] = vobj
+            if f4 is not None:
+                line["threshold_decrypt"] = f4
         else:
             line = {
                 "metric": METRIC, "value": vobj["value"], "unit": "GB/s", "n_gpus": world,

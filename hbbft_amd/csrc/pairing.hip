@@ -30,6 +30,8 @@
 // line is scaled into the sparse form (c0, c1, c4) and applied with
 // mul_by_014; f is conjugated at the end (x < 0).  Final exponentiation: easy
 // part, then the crate's hard-part chain (= f^(3 (p^4 - p^2 + 1)/r)).
+#include <cstdlib>
+
 #include "bls_consts.hpp"
 #include "device_common.hpp"
 #include "launchers.hpp"
@@ -48,6 +50,13 @@ struct Fp6 { Fp2 c0, c1, c2; };
 struct Fp12 { Fp6 c0, c1; };
 
 #define DEV __device__ __forceinline__
+// Call boundaries of the big tower products (HB_PAIR_INLINE=1 inlines them
+// too; measured in DESIGN.md §6e).
+#if defined(HB_PAIR_INLINE) && HB_PAIR_INLINE
+#define NOINL __device__ __forceinline__
+#else
+#define NOINL __device__ __noinline__
+#endif
 
 // ---------------------------------------------------------------- Fp
 DEV void fp_set(Fp &r, const uint32_t (&v)[NL]) {
@@ -74,49 +83,41 @@ DEV bool fp_eq(const Fp &a, const Fp &b) {
     return t == 0;
 }
 
+// 32-bit add / subtract with carry (v_add_co_ci_u32 / v_sub_co_ci_u32 chains)
+DEV uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t *cout) {
+    return __builtin_addc(a, b, cin, cout);
+}
+DEV uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t *bout) {
+    return __builtin_subc(a, b, bin, bout);
+}
+
 // r = t - p if t >= p else t  (t < 2p)
 DEV void fp_reduce_once(Fp &r, const uint32_t (&t)[NL]) {
     uint32_t s[NL];
-    uint64_t br = 0;
+    uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        const uint64_t d = (uint64_t)t[i] - kP[i] - br;
-        s[i] = (uint32_t)d;
-        br = (d >> 32) & 1u;
-    }
+    for (int i = 0; i < NL; ++i) s[i] = subb(t[i], kP[i], br, &br);
 #pragma unroll
     for (int i = 0; i < NL; ++i) r.l[i] = br ? t[i] : s[i];
 }
 
 DEV void fp_add(Fp &r, const Fp &a, const Fp &b) {
     uint32_t t[NL];
-    uint64_t c = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        c += (uint64_t)a.l[i] + b.l[i];
-        t[i] = (uint32_t)c;
-        c >>= 32;
-    }
+    for (int i = 0; i < NL; ++i) t[i] = addc(a.l[i], b.l[i], c, &c);
     fp_reduce_once(r, t);  // a + b < 2p < 2^382: no carry out of limb 11
 }
 
 DEV void fp_sub(Fp &r, const Fp &a, const Fp &b) {
     uint32_t t[NL];
-    uint64_t br = 0;
+    uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        const uint64_t d = (uint64_t)a.l[i] - b.l[i] - br;
-        t[i] = (uint32_t)d;
-        br = (d >> 32) & 1u;
-    }
-    const uint32_t mask = 0u - (uint32_t)br;  // add p back on borrow
-    uint64_t c = 0;
+    for (int i = 0; i < NL; ++i) t[i] = subb(a.l[i], b.l[i], br, &br);
+    const uint32_t mask = 0u - br;  // add p back on borrow
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        c += (uint64_t)t[i] + (kP[i] & mask);
-        r.l[i] = (uint32_t)c;
-        c >>= 32;
-    }
+    for (int i = 0; i < NL; ++i) r.l[i] = addc(t[i], kP[i] & mask, c, &c);
 }
 
 DEV void fp_dbl(Fp &r, const Fp &a) { fp_add(r, a, a); }
@@ -127,32 +128,49 @@ DEV void fp_neg(Fp &r, const Fp &a) {
     fp_sub(r, z, a);
 }
 
-// Montgomery product a*b*2^-384 mod p, CIOS over 32-bit limbs.  p < 2^381,
-// so the running value stays below 2p < 2^382 and one extra word holds every
-// carry (the top limb of p leaves three spare bits).
+// One Montgomery step of CIOS: t <- (t + m p) / 2^32 with m = t0 * (-p^-1).
+// The 12 products m*p_j + t_j are independent (v_mad_u64_u32 with the limb as
+// addend); their high halves ride one add-with-carry chain.
+DEV void mont_step(uint32_t (&t)[NL + 1]) {
+    const uint32_t m = t[0] * kInv32;
+    uint64_t q[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) q[j] = (uint64_t)m * kP[j] + t[j];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 1; j < NL; ++j) t[j - 1] = addc((uint32_t)q[j], (uint32_t)(q[j - 1] >> 32), c, &c);
+    t[NL - 1] = addc(t[NL], (uint32_t)(q[NL - 1] >> 32), c, &c);
+    t[NL] = c;
+}
+
+// Montgomery product a*b*2^-384 mod p, CIOS over 32-bit limbs (p < 2^381, so
+// the running value stays below 2p and one extra word holds every carry).
+// Per row: 12 independent a_j*b_i + t_j products, one carry chain over their
+// high halves, one Montgomery step -- two VALU per limb product.
 DEV void fp_mul(Fp &r, const Fp &a, const Fp &b) {
     uint32_t t[NL + 1];
+    {
+        uint64_t p[NL];
 #pragma unroll
-    for (int i = 0; i <= NL; ++i) t[i] = 0;
+        for (int j = 0; j < NL; ++j) p[j] = (uint64_t)a.l[j] * b.l[0];
+        uint32_t c = 0;
+        t[0] = (uint32_t)p[0];
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        uint64_t c = 0;
+        for (int j = 1; j < NL; ++j) t[j] = addc((uint32_t)p[j], (uint32_t)(p[j - 1] >> 32), c, &c);
+        t[NL] = (uint32_t)(p[NL - 1] >> 32) + c;
+        mont_step(t);
+    }
 #pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            c = (uint64_t)a.l[j] * b.l[i] + t[j] + (c >> 32);
-            t[j] = (uint32_t)c;
-        }
-        t[NL] += (uint32_t)(c >> 32);
-        const uint32_t m = t[0] * kInv32;
-        c = (uint64_t)m * kP[0] + t[0];
+    for (int i = 1; i < NL; ++i) {
+        uint64_t p[NL];
 #pragma unroll
-        for (int j = 1; j < NL; ++j) {
-            c = (uint64_t)m * kP[j] + t[j] + (c >> 32);
-            t[j - 1] = (uint32_t)c;
-        }
-        c = (uint64_t)t[NL] + (c >> 32);
-        t[NL - 1] = (uint32_t)c;
-        t[NL] = (uint32_t)(c >> 32);
+        for (int j = 0; j < NL; ++j) p[j] = (uint64_t)a.l[j] * b.l[i] + t[j];
+        uint32_t c = 0;
+        t[0] = (uint32_t)p[0];
+#pragma unroll
+        for (int j = 1; j < NL; ++j) t[j] = addc((uint32_t)p[j], (uint32_t)(p[j - 1] >> 32), c, &c);
+        t[NL] = t[NL] + (uint32_t)(p[NL - 1] >> 32) + c;
+        mont_step(t);
     }
     uint32_t u[NL];
 #pragma unroll
@@ -187,7 +205,7 @@ DEV void fp2_zero(Fp2 &r) { fp_zero(r.c0); fp_zero(r.c1); }
 DEV bool fp2_is_zero(const Fp2 &a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 DEV bool fp2_eq(const Fp2 &a, const Fp2 &b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
 
-__device__ __noinline__ void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+NOINL void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     Fp t0, t1, s0, s1;
     fp_mul(t0, a.c0, b.c0);
     fp_mul(t1, a.c1, b.c1);
@@ -199,7 +217,7 @@ __device__ __noinline__ void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     fp_sub(r.c1, s0, t1);
 }
 
-__device__ __noinline__ void fp2_sqr(Fp2 &r, const Fp2 &a) {
+NOINL void fp2_sqr(Fp2 &r, const Fp2 &a) {
     Fp s, d, m;
     fp_add(s, a.c0, a.c1);
     fp_sub(d, a.c0, a.c1);
@@ -252,7 +270,7 @@ DEV void fp6_mul_v(Fp6 &r, const Fp6 &a) {
     r.c0 = t;
 }
 
-__device__ __noinline__ void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
+NOINL void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
     Fp2 aa, bb, cc, s, t, t1, t2, t3;
     fp2_mul(aa, a.c0, b.c0);
     fp2_mul(bb, a.c1, b.c1);
@@ -373,7 +391,7 @@ DEV bool fp12_is_one(const Fp12 &a) {
 
 DEV void fp12_conj(Fp12 &r, const Fp12 &a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
 
-__device__ __noinline__ void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) {
+NOINL void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) {
     Fp6 aa, bb, s, t;
     fp6_mul(aa, a.c0, b.c0);
     fp6_mul(bb, a.c1, b.c1);
@@ -386,7 +404,7 @@ __device__ __noinline__ void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) {
     fp6_add(r.c0, aa, bb);
 }
 
-__device__ __noinline__ void fp12_sqr(Fp12 &r, const Fp12 &a) {
+NOINL void fp12_sqr(Fp12 &r, const Fp12 &a) {
     Fp6 ab, s, t;
     fp6_mul(ab, a.c0, a.c1);
     fp6_add(s, a.c0, a.c1);
@@ -400,7 +418,7 @@ __device__ __noinline__ void fp12_sqr(Fp12 &r, const Fp12 &a) {
 }
 
 // f * (c0 + c1 v + c4 v w): the sparse line value
-__device__ __noinline__ void fp12_mul_by_014(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4) {
+NOINL void fp12_mul_by_014(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4) {
     Fp6 aa, bb, s;
     Fp2 o;
     fp6_mul_by_01(aa, f.c0, c0, c1);
@@ -426,7 +444,7 @@ DEV void fp12_inv(Fp12 &r, const Fp12 &a) {
     fp6_neg(r.c1, t1);
 }
 
-__device__ __noinline__ void fp12_frob(Fp12 &r, const Fp12 &a, int k) {
+NOINL void fp12_frob(Fp12 &r, const Fp12 &a, int k) {
     Fp6 c1;
     Fp2 g;
     fp6_frob(r.c0, a.c0, k);
@@ -437,13 +455,57 @@ __device__ __noinline__ void fp12_frob(Fp12 &r, const Fp12 &a, int k) {
     fp2_mul(r.c1.c2, c1.c2, g);
 }
 
+// (a + b s)^2 in Fp4 = Fp2[s]/(s^2 - xi): (a^2 + xi b^2, 2ab)
+DEV void fp4_sqr(Fp2 &c0, Fp2 &c1, const Fp2 &a, const Fp2 &b) {
+    Fp2 t0, t1, t2;
+    fp2_sqr(t0, a);
+    fp2_sqr(t1, b);
+    fp2_mul_xi(t2, t1);
+    fp2_add(c0, t2, t0);
+    fp2_add(t2, a, b);
+    fp2_sqr(t2, t2);
+    fp2_sub(t2, t2, t0);
+    fp2_sub(c1, t2, t1);
+}
+
+// Granger-Scott squaring, valid on the cyclotomic subgroup (every value of
+// the hard part): 9 Fp2 squarings instead of the 2 Fp6 products of fp12_sqr.
+NOINL void fp12_cyclo_sqr(Fp12 &f) {
+    Fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+    Fp2 t0, t1, t2, t3;
+    fp4_sqr(t0, t1, z0, z1);
+    fp2_sub(z0, t0, z0);
+    fp2_dbl(z0, z0);
+    fp2_add(z0, z0, t0);          // 3 t0 - 2 z0
+    fp2_add(z1, t1, z1);
+    fp2_dbl(z1, z1);
+    fp2_add(z1, z1, t1);          // 3 t1 + 2 z1
+    fp4_sqr(t0, t1, z2, z3);
+    fp4_sqr(t2, t3, z4, z5);
+    fp2_sub(z4, t0, z4);
+    fp2_dbl(z4, z4);
+    fp2_add(z4, z4, t0);
+    fp2_add(z5, t1, z5);
+    fp2_dbl(z5, z5);
+    fp2_add(z5, z5, t1);
+    fp2_mul_xi(t0, t3);
+    fp2_add(z2, t0, z2);
+    fp2_dbl(z2, z2);
+    fp2_add(z2, z2, t0);
+    fp2_sub(z3, t2, z3);
+    fp2_dbl(z3, z3);
+    fp2_add(z3, z3, t2);
+    f.c0.c0 = z0; f.c0.c1 = z4; f.c0.c2 = z3;
+    f.c1.c0 = z2; f.c1.c1 = z1; f.c1.c2 = z5;
+}
+
 // f^x for the BLS parameter x < 0 (the crate's exp_by_x: pow by |x|, then
 // conjugate -- the inverse on the cyclotomic subgroup).  `shift` gives |x|>>1.
-__device__ __noinline__ void fp12_exp_by_x(Fp12 &r, const Fp12 &a, int shift) {
+NOINL void fp12_exp_by_x(Fp12 &r, const Fp12 &a, int shift) {
     const uint64_t e = kXAbs >> shift;
     Fp12 acc = a;
     for (int b = 62 - shift; b >= 0; --b) {
-        fp12_sqr(acc, acc);
+        fp12_cyclo_sqr(acc);
         if ((e >> b) & 1u) fp12_mul(acc, acc, a);
     }
     fp12_conj(r, acc);
@@ -621,7 +683,8 @@ constexpr int kPairBlock = 64;
 // point g2[i]; with `negate_odd`, odd pairings negate their G1 point (the
 // c of a check a,b == c,d sits at pairing 2i+1).  status[i] gets the point
 // status (max of the two); an infinity or invalid input leaves f = 1.
-__global__ __launch_bounds__(kPairBlock) void miller_kernel(
+template <int W>
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(W, W))) void miller_kernel(
     const uint8_t *__restrict__ g1, size_t g1_stride, const uint8_t *__restrict__ g2,
     size_t g2_stride, size_t n, int pair_inputs, uint32_t *__restrict__ ws,
     uint8_t *__restrict__ status) {
@@ -705,7 +768,8 @@ DEV void store_be48(uint8_t *dst, const Fp &a) {
 // (1: a pairing, 2: a check) are multiplied first.  gt_out (if set) gets the
 // 576-byte GT value; ok_out (if set) gets 1 if the value is 1 (the check
 // holds), 0 if not, 2 if an input point was invalid.
-__global__ __launch_bounds__(kPairBlock) void final_exp_kernel(
+template <int W>
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(W, W))) void final_exp_kernel(
     const uint32_t *__restrict__ ws, size_t n_miller, size_t n_out, int per_out,
     const uint8_t *__restrict__ status, uint8_t *__restrict__ gt_out,
     uint8_t *__restrict__ ok_out) {
@@ -737,13 +801,27 @@ __global__ __launch_bounds__(kPairBlock) void final_exp_kernel(
 
 }  // namespace
 
+// Waves per SIMD the kernels are compiled for (register budget 512 / W per
+// lane; the rest spills to scratch).  HBRBC_PAIR_WAVES=1|2|4 picks one for
+// A/B runs; the default is the measured best.
+static int pair_waves() {
+    static int w = [] {
+        const char *e = getenv("HBRBC_PAIR_WAVES");
+        const int v = e ? atoi(e) : 4;
+        return (v == 1 || v == 2 || v == 4) ? v : 4;
+    }();
+    return w;
+}
+
 hipError_t launch_pairing_miller(const uint8_t *g1, size_t g1_stride, const uint8_t *g2,
                                  size_t g2_stride, size_t n, int pair_inputs, uint32_t *ws,
                                  uint8_t *status, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n + kPairBlock - 1) / kPairBlock);
-    hipLaunchKernelGGL(miller_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, g1_stride, g2,
-                       g2_stride, n, pair_inputs, ws, status);
+    const int w = pair_waves();
+    auto k = w == 1 ? miller_kernel<1> : w == 2 ? miller_kernel<2> : miller_kernel<4>;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kPairBlock), 0, s, g1, g1_stride, g2, g2_stride, n,
+                       pair_inputs, ws, status);
     return hipGetLastError();
 }
 
@@ -752,8 +830,10 @@ hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_ou
                                 hipStream_t s) {
     if (n_out == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n_out + kPairBlock - 1) / kPairBlock);
-    hipLaunchKernelGGL(final_exp_kernel, dim3(blocks), dim3(kPairBlock), 0, s, ws, n_miller,
-                       n_out, per_out, status, gt_out, ok_out);
+    const int w = pair_waves();
+    auto k = w == 1 ? final_exp_kernel<1> : w == 2 ? final_exp_kernel<2> : final_exp_kernel<4>;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(kPairBlock), 0, s, ws, n_miller, n_out, per_out,
+                       status, gt_out, ok_out);
     return hipGetLastError();
 }
 

@@ -37,8 +37,18 @@ def main():
         checks.append({"a": B.g1_bytes(share).hex(), "b": B.g2_bytes(H).hex(),
                        "c": B.g1_bytes(pk).hex(), "d": B.g2_bytes(W).hex(),
                        "expect": not tamper, "kind": "verify_decryption_share"})
+    # bench pool (bench.py's f4 leg tiles these): 32 checks, one in four tampered
+    import random
+    rng = random.Random(0x48424246)
+    pool = []
+    for i in range(32):
+        share, H, pk, W = B.decryption_share_case(rng.randrange(1, B.R), rng.randrange(1, B.R),
+                                                  rng.randrange(1, B.R), tamper=(i % 4 == 3))
+        pool.append({"a": B.g1_bytes(share).hex(), "b": B.g2_bytes(H).hex(),
+                     "c": B.g1_bytes(pk).hex(), "d": B.g2_bytes(W).hex(),
+                     "expect": i % 4 != 3, "kind": "verify_decryption_share"})
     out = {"source": "oracle/bls_oracle.py (restatement of the pairing crate's BLS12-381)",
-           "pairings": vectors, "checks": checks}
+           "pairings": vectors, "checks": checks, "bench_pool": pool}
     path = os.path.join(ROOT, "tests", "golden", "bls_vectors.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
