@@ -585,7 +585,7 @@ def f4_cpu_baseline(pool, reps):
     cpus = len(os.sched_getaffinity(0))
     quota = cpu_quota()
     procs = max(1, min(cpus, int(quota)) if quota else cpus)
-    items = [pool[i % len(pool)] for i in range(2 * procs)]
+    items = [pool[i % len(pool)] for i in range(24 * procs)]   # ~3 s per rep
     times = []
     with mp.get_context("spawn").Pool(procs) as p:
         p.map(f4_cpu_check, items[:procs])                      # warm-up / import

@@ -63,6 +63,11 @@ __global__ __launch_bounds__(256) void op_loop(uint32_t *out, int iters, uint32_
                 if constexpr (KIND == 21) asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(a[i]) : "v"(b));
                 if constexpr (KIND == 22) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(b));
                 if constexpr (KIND == 23) asm volatile("v_pk_add_u16 %0, %0, %0" : "+v"(a[i]));
+                // multi-precision pieces of the BLS12-381 Fp product (pairing.hip)
+                if constexpr (KIND == 24)
+                    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(*(uint64_t *)&a[i & 14]) : "v"(b), "v"(c) : "vcc");
+                if constexpr (KIND == 25) asm volatile("v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a[i]) : "v"(b) : "vcc");
+                if constexpr (KIND == 26) asm volatile("v_mov_b32 %0, %1" : "=v"(a[i]) : "v"(a[(i + 1) & 15]));
             }
         }
     }
@@ -111,16 +116,17 @@ int main() {
     const int blocks = cus * 8 * 16;  // many full rounds of residency
     CHECK(hipMalloc(&out, (size_t)blocks * 256 * 4));
     const int iters = 64;
-    const char *names[24] = {"v_xor_b32", "v_bitop3_b32", "v_alignbit_b32(v,v)", "v_perm_b32(s,s,v)",
+    const char *names[27] = {"v_xor_b32", "v_bitop3_b32", "v_alignbit_b32(v,v)", "v_perm_b32(s,s,v)",
                              "v_and_b32", "v_lshl_or_b32", "v_alignbit_b32(s,v)", "v_perm_b32(v,v,v)",
                              "v_pk_mov_b32", "v_lshrrev_b32", "v_alignbyte_b32", "v_add_u32",
                              "v_lshrrev_b64", "v_lshl_add_u64", "v_lshlrev_b32", "v_or3_b32",
                              "v_xor_b32 (x^0)", "v_alignbit_b32 (0)", "v_lshrrev_b32 (b)", "v_lshlrev_b32 (b)",
-                             "v_pk_lshlrev_b16", "v_lshl_add_u32", "v_mul_u32_u24", "v_pk_add_u16"};
+                             "v_pk_lshlrev_b16", "v_lshl_add_u32", "v_mul_u32_u24", "v_pk_add_u16",
+                             "v_mad_u64_u32", "v_addc_co_u32 (vcc chain)", "v_mov_b32"};
 #define K(n) case n: hipLaunchKernelGGL(op_loop<n>, dim3(blocks), dim3(256), 0, 0, out, iters, 1u); break
-    for (int kind = 0; kind < 24; ++kind) {
+    for (int kind = 0; kind < 27; ++kind) {
         float ms = time_ms([&] {
-            switch (kind) { K(0); K(1); K(2); K(3); K(4); K(5); K(6); K(7); K(8); K(9); K(10); K(11); K(12); K(13); K(14); K(15); K(16); K(17); K(18); K(19); K(20); K(21); K(22); K(23); }
+            switch (kind) { K(0); K(1); K(2); K(3); K(4); K(5); K(6); K(7); K(8); K(9); K(10); K(11); K(12); K(13); K(14); K(15); K(16); K(17); K(18); K(19); K(20); K(21); K(22); K(23); K(24); K(25); K(26); }
         });
         const double instr = (double)blocks * 256 * iters * 8 * 16;
         printf("%-22s %8.3f ms  %6.2f T lane-instr/s\n", names[kind], ms, instr / ms / 1e9);
