@@ -456,9 +456,23 @@ int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, const RowM
 hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, XorArgs a,
                             size_t count, hipStream_t s);
 
+// Fused unframe (decode paths): the generic reconstruct kernel writes the
+// payload bytes of the data rows it reads or rebuilds, so unframe's re-read of
+// k*S bytes per instance disappears (decode_check + a zero-fill fixup remain).
+// Needs S % 4 == 0 (dword-aligned destinations) and no pattern-specialised
+// decoder in the call; HBRBC_UNFRAME_FUSED=0 keeps the separate unframe (A/B).
+bool unframe_fusable(const hbrbc_ctx *c, size_t shard_len, size_t payload_stride) {
+    const char *e = getenv("HBRBC_UNFRAME_FUSED");
+    if (e && !std::strcmp(e, "0")) return false;
+    return c->m > 0 && shard_len % 4 == 0 && payload_stride % 16 == 0 &&
+           (uint64_t)c->k * shard_len > 4;
+}
+
 int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &rows,
                     size_t inst_stride, const uint8_t *present, size_t count, int32_t *status,
-                    hipStream_t s) {
+                    hipStream_t s, uint8_t *uf_payload = nullptr, size_t uf_stride = 0,
+                    bool *fused_out = nullptr) {
+    if (fused_out) *fused_out = false;
     int st = ensure_workspace(c, count);
     if (st) return st;
     // rse keeps an LRU of decode matrices; here the shared slots are flushed
@@ -525,6 +539,14 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
     g.rt = c->rt_rec;
     g.mode = c->gf_mode;
     g.count = count;
+    if (uf_payload && !spec) {
+        g.payload = uf_payload;
+        g.payload_stride = uf_stride;
+        g.payload_S = (uint32_t)shard_len;
+        g.payload_k = (uint32_t)c->k;
+        g.rstatus = status;
+        if (fused_out) *fused_out = true;
+    }
     HB_HIP(launch_gf_apply(g, s));
     return HBRBC_OK;
 }
@@ -842,7 +864,10 @@ int decode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &r
     int st = ensure_workspace(c, count);
     if (st) return st;
     int32_t *rstat = c->ws_status.as<int32_t>();
-    st = run_reconstruct(c, shards, shard_len, rows, inst_stride, present, count, rstat, s);
+    bool fused = false;
+    const bool fusable = unframe_fusable(c, shard_len, payload_stride);
+    st = run_reconstruct(c, shards, shard_len, rows, inst_stride, present, count, rstat, s,
+                         fusable ? payload_out : nullptr, payload_stride, &fused);
     if (st) return st;
     st = run_merkle(c, shards, shard_len, rows, inst_stride, c->n, count, nodes, node_inst_stride,
                     known_leaves, s);
@@ -851,8 +876,12 @@ int decode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &r
     HB_HIP(launch_decode_check(rstat, nodes, node_inst_stride, hbrbc_merkle_node_count(c->n) - 1,
                                roots, root_stride, shards, shard_len, rows, inst_stride, c->k,
                                count, payload_len_out, status_out, s));
-    HB_HIP(launch_unframe(shards, shard_len, rows, inst_stride, c->k, count, payload_len_out,
-                          status_out, payload_out, payload_stride, s));
+    if (fused)
+        HB_HIP(launch_unframe_fixup((uint32_t)shard_len, (uint32_t)c->k, count, payload_len_out,
+                                    status_out, payload_out, payload_stride, s));
+    else
+        HB_HIP(launch_unframe(shards, shard_len, rows, inst_stride, c->k, count, payload_len_out,
+                              status_out, payload_out, payload_stride, s));
     return HBRBC_OK;
 }
 

@@ -212,6 +212,27 @@ __device__ __forceinline__ void bs_transpose(uint32_t (&w)[8]) {
     }
 }
 
+// Fused unframe (decode_from_shards, broadcast.rs:590-598): 16 bytes of data
+// row `row` at byte `pos` are payload bytes row*S + pos - 4 .. +15 (S % 4 == 0,
+// so every destination is dword-aligned; unaligned-access mode stores 16 B at
+// once).  Bytes of the row padding (pos >= S) and the 4-byte length prefix are
+// not payload.  The fixup after the root check zero-fills past the length.
+typedef uint32_t hb_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void unframe_put(uint8_t *pb, uint32_t S, uint32_t row, uint32_t pos,
+                                            uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if (pos >= S) return;
+    const int64_t dst = (int64_t)row * S + pos - 4;
+    if (dst >= 0 && pos + 16 <= S) {
+        *reinterpret_cast<hb_u32x4_a4 *>(pb + dst) = (hb_u32x4_a4){a, b, c, d};
+        return;
+    }
+    const uint32_t w[4] = {a, b, c, d};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (pos + 4 * q < S && dst + 4 * q >= 0)
+            *reinterpret_cast<uint32_t *>(pb + dst + 4 * q) = w[q];
+}
+
 template <int RT, int MODE>
 // Workgroup = up to 4 waves over the SAME 2048 positions; wave w produces
 // passes w, w + nwaves, ...  The waves read identical input bytes at the
@@ -226,7 +247,8 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
     const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
     const int *__restrict__ nout_arr, int nout_uniform, const int *__restrict__ pat,
     const uint64_t *__restrict__ slot_hash, uint64_t skip_hash, int hash_slots, int nin,
-    uint32_t waves_per_row, uint32_t piece) {
+    uint32_t waves_per_row, uint32_t piece, uint8_t *__restrict__ uf_payload, size_t uf_stride,
+    uint32_t uf_S, uint32_t uf_k, const int32_t *__restrict__ uf_status) {
     const size_t inst = blockIdx.x / waves_per_row;
     const int slot = pat ? pat[inst] : (int)inst;
     // instances of a pattern with a specialised decoder are left to it
@@ -250,6 +272,21 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
     // vmcnt(0) drained the prefetch pipeline)
     const uint32_t *iidx = in_idx + (size_t)slot * in_idx_stride;
     const uint32_t *oidx = out_idx + (size_t)slot * out_idx_stride;
+    // fused unframe: payload bytes of the data rows this launch reads (pass 0)
+    // or rebuilds; instances whose reconstruct failed are left to the fixup
+    uint8_t *ufp = (uf_payload && uf_status[inst] == 0) ? uf_payload + inst * uf_stride : nullptr;
+    if (ufp && npass == 0 && wave == 0 && active) {
+        // nothing to rebuild: the data rows are rows 0..k-1 as they are
+        for (uint32_t r = 0; r < uf_k; ++r) {
+            const uint8_t *src = ib + rows.off(r) + off;
+            const uint4 l = *reinterpret_cast<const uint4 *>(src);
+            unframe_put(ufp, uf_S, r, off, l.x, l.y, l.z, l.w);
+            if (full) {
+                const uint4 h = *reinterpret_cast<const uint4 *>(src + d2);
+                unframe_put(ufp, uf_S, r, off + d2, h.x, h.y, h.z, h.w);
+            }
+        }
+    }
     for (int p = __builtin_amdgcn_readfirstlane(wave); p < npass; p += nwaves) {
         uint32_t acc[RT][8];
 #pragma unroll
@@ -270,6 +307,13 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
         };
         auto consume = [&](int jj, const uint4 &lo, const uint4 &h) {
             const uint4 hi = full ? h : make_uint4(0, 0, 0, 0);
+            if (ufp && p == 0) {
+                const uint32_t r = iidx[jj];
+                if (r < uf_k && active) {
+                    unframe_put(ufp, uf_S, r, off, lo.x, lo.y, lo.z, lo.w);
+                    if (full) unframe_put(ufp, uf_S, r, off + d2, hi.x, hi.y, hi.z, hi.w);
+                }
+            }
             uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             bs_transpose(x);
             // RT coefficient bytes of input jj for this pass (16-byte padded, scalar load)
@@ -315,9 +359,16 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
             for (int t = 0; t < RT; ++t) {
                 if (p * RT + t < nout) {
                     bs_transpose(acc[t]);
-                    uint8_t *dst = ib + rows.off(oidx[p * RT + t]) + off;
+                    const uint32_t orow = oidx[p * RT + t];
+                    uint8_t *dst = ib + rows.off(orow) + off;
                     store16_stream(dst, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
                     if (full) store16_stream(dst + d2, acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
+                    if (ufp && orow < uf_k) {
+                        unframe_put(ufp, uf_S, orow, off, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+                        if (full)
+                            unframe_put(ufp, uf_S, orow, off + d2, acc[t][4], acc[t][5], acc[t][6],
+                                        acc[t][7]);
+                    }
                 }
             }
         }
@@ -966,7 +1017,7 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
                        s, a.base, a.inst_stride, a.rows, row_bytes, a.coefs, a.coef_slot_stride, \
                        a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,          \
                        a.nout_uniform, a.pat, a.slot_hash, a.skip_hash, a.hash_slots, a.nin, wpr,   \
-                       piece)
+                       piece, a.payload, a.payload_stride, a.payload_S, a.payload_k, a.rstatus)
 #define HB_BS_CASE(RT)                                                                           \
     case RT:                                                                                     \
         if (a.mode == 2)                                                                         \
@@ -1130,6 +1181,49 @@ hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes
                        0, s, recon_status, nodes, node_inst_stride, (uint32_t)root_node, roots,
                        root_stride, shards, (uint32_t)shard_len, rows, inst_stride,
                        (uint32_t)data_shards, count, plen_out, status_out);
+    return hipGetLastError();
+}
+
+// Fixup after a fused-unframe reconstruct (gf_bitslice_kernel wrote payload
+// bytes [0, k*S - 4) of every instance whose reconstruct succeeded): zero the
+// bytes past the decoded length, or the whole slot of a failed instance, so
+// the payload buffer ends exactly as unframe_kernel leaves it.  One workgroup
+// per instance; honest instances touch one or two chunks.
+__global__ __launch_bounds__(kBlock) void unframe_fixup_kernel(
+    uint32_t chunks, const uint32_t *__restrict__ plen, const int32_t *__restrict__ status,
+    uint8_t *__restrict__ payload_out, size_t payload_stride) {
+    const size_t inst = blockIdx.x;
+    const uint32_t len = status[inst] == 0 ? plen[inst] : 0u;
+    uint8_t *pb = payload_out + inst * payload_stride;
+    for (uint32_t c = len / 16 + threadIdx.x; c < chunks; c += kBlock) {
+        const uint32_t o = c * 16;
+        uint4 *dst = reinterpret_cast<uint4 *>(pb + o);
+        if (o >= len) {
+            *dst = make_uint4(0, 0, 0, 0);
+        } else {
+            uint4 v = *dst;
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t nb = len - o;   // 1..15 payload bytes in this chunk
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int keep = (int)nb - 4 * q;
+                if (keep <= 0) w[q] = 0;
+                else if (keep < 4) w[q] &= (1u << (8 * keep)) - 1u;
+            }
+            *dst = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
+hipError_t launch_unframe_fixup(uint32_t S, uint32_t k, size_t count, const uint32_t *plen,
+                                const int32_t *status, uint8_t *payload_out, size_t payload_stride,
+                                hipStream_t s) {
+    const uint64_t total = (uint64_t)k * S;
+    if (count == 0 || total <= 4) return hipSuccess;
+    if (count > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t chunks = (uint32_t)((total - 4 + 15) / 16);
+    hipLaunchKernelGGL(unframe_fixup_kernel, dim3((unsigned)count), dim3(kBlock), 0, s, chunks,
+                       plen, status, payload_out, payload_stride);
     return hipGetLastError();
 }
 

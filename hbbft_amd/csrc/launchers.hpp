@@ -72,6 +72,11 @@ struct GfApplyArgs {
     int rt;                     // rows per pass: one of 2,4,...,16
     int mode;                   // 0 branch per coefficient bit, 1 branch hinted, 2 masked
     size_t count;
+    // fused unframe (reconstruct): payload bytes of the data rows, payload_S % 4 == 0
+    uint8_t *payload = nullptr;
+    size_t payload_stride = 0;
+    uint32_t payload_S = 0, payload_k = 0;
+    const int32_t *rstatus = nullptr;   // reconstruct status per instance (0 = ok)
 };
 // Row tile for `rows` output rows: fewest passes of <= 16, evened out.
 int gf_row_tile(int rows);
@@ -170,6 +175,11 @@ hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes
                                const RowMap &rows, size_t inst_stride, size_t data_shards,
                                size_t count, uint32_t *plen_out, int32_t *status_out,
                                hipStream_t s);
+// After a fused-unframe reconstruct: zero payload bytes past the decoded
+// length (all of them for a failed instance), as unframe_kernel leaves them.
+hipError_t launch_unframe_fixup(uint32_t S, uint32_t k, size_t count, const uint32_t *plen,
+                                const int32_t *status, uint8_t *payload_out, size_t payload_stride,
+                                hipStream_t s);
 hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, const RowMap &rows,
                           size_t inst_stride, size_t data_shards, size_t count,
                           const uint32_t *plen, const int32_t *status, uint8_t *payload_out,
