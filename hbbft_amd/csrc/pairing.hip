@@ -50,13 +50,9 @@ struct Fp6 { Fp2 c0, c1, c2; };
 struct Fp12 { Fp6 c0, c1; };
 
 #define DEV __device__ __forceinline__
-// Call boundaries of the big tower products (HB_PAIR_INLINE=1 inlines them
-// too; measured in DESIGN.md §6e).
-#if defined(HB_PAIR_INLINE) && HB_PAIR_INLINE
-#define NOINL __device__ __forceinline__
-#else
+// Call boundaries: out-of-line units keep compile time bounded; everything
+// below an NOINL unit is inlined into it.
 #define NOINL __device__ __noinline__
-#endif
 
 // ---------------------------------------------------------------- Fp
 DEV void fp_set(Fp &r, const uint32_t (&v)[NL]) {
@@ -205,7 +201,7 @@ DEV void fp2_zero(Fp2 &r) { fp_zero(r.c0); fp_zero(r.c1); }
 DEV bool fp2_is_zero(const Fp2 &a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 DEV bool fp2_eq(const Fp2 &a, const Fp2 &b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
 
-NOINL void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     Fp t0, t1, s0, s1;
     fp_mul(t0, a.c0, b.c0);
     fp_mul(t1, a.c1, b.c1);
@@ -217,7 +213,7 @@ NOINL void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     fp_sub(r.c1, s0, t1);
 }
 
-NOINL void fp2_sqr(Fp2 &r, const Fp2 &a) {
+DEV void fp2_sqr_in(Fp2 &r, const Fp2 &a) {
     Fp s, d, m;
     fp_add(s, a.c0, a.c1);
     fp_sub(d, a.c0, a.c1);
@@ -225,6 +221,12 @@ NOINL void fp2_sqr(Fp2 &r, const Fp2 &a) {
     fp_mul(r.c0, s, d);
     fp_dbl(r.c1, m);
 }
+
+// Out-of-line forms for cold code (inversions, Frobenius, input checks); the
+// hot units (Fp6 products, the sparse line product, the cyclotomic square, the
+// Miller steps) inline fp2_mul_in / fp2_sqr_in into their own bodies.
+NOINL void fp2_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp2_mul_in(r, a, b); }
+NOINL void fp2_sqr(Fp2 &r, const Fp2 &a) { fp2_sqr_in(r, a); }
 
 DEV void fp2_mul_fp(Fp2 &r, const Fp2 &a, const Fp &s) { fp_mul(r.c0, a.c0, s); fp_mul(r.c1, a.c1, s); }
 
@@ -272,25 +274,25 @@ DEV void fp6_mul_v(Fp6 &r, const Fp6 &a) {
 
 NOINL void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
     Fp2 aa, bb, cc, s, t, t1, t2, t3;
-    fp2_mul(aa, a.c0, b.c0);
-    fp2_mul(bb, a.c1, b.c1);
-    fp2_mul(cc, a.c2, b.c2);
+    fp2_mul_in(aa, a.c0, b.c0);
+    fp2_mul_in(bb, a.c1, b.c1);
+    fp2_mul_in(cc, a.c2, b.c2);
     fp2_add(s, a.c1, a.c2);
     fp2_add(t, b.c1, b.c2);
-    fp2_mul(t1, s, t);
+    fp2_mul_in(t1, s, t);
     fp2_sub(t1, t1, bb);
     fp2_sub(t1, t1, cc);
     fp2_mul_xi(t1, t1);
     fp2_add(t1, t1, aa);
     fp2_add(s, a.c0, a.c2);
     fp2_add(t, b.c0, b.c2);
-    fp2_mul(t3, s, t);
+    fp2_mul_in(t3, s, t);
     fp2_sub(t3, t3, aa);
     fp2_add(t3, t3, bb);
     fp2_sub(t3, t3, cc);
     fp2_add(s, a.c0, a.c1);
     fp2_add(t, b.c0, b.c1);
-    fp2_mul(t2, s, t);
+    fp2_mul_in(t2, s, t);
     fp2_sub(t2, t2, aa);
     fp2_sub(t2, t2, bb);
     fp2_mul_xi(cc, cc);
@@ -303,21 +305,21 @@ NOINL void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
 // (a0 + a1 v + a2 v^2)(c0 + c1 v)
 DEV void fp6_mul_by_01(Fp6 &r, const Fp6 &a, const Fp2 &c0, const Fp2 &c1) {
     Fp2 aa, bb, s, t1, t2, t3;
-    fp2_mul(aa, a.c0, c0);
-    fp2_mul(bb, a.c1, c1);
+    fp2_mul_in(aa, a.c0, c0);
+    fp2_mul_in(bb, a.c1, c1);
     fp2_add(s, a.c1, a.c2);
-    fp2_mul(t1, s, c1);
+    fp2_mul_in(t1, s, c1);
     fp2_sub(t1, t1, bb);
     fp2_mul_xi(t1, t1);
     fp2_add(t1, t1, aa);
     fp2_add(s, a.c0, a.c2);
-    fp2_mul(t3, s, c0);
+    fp2_mul_in(t3, s, c0);
     fp2_sub(t3, t3, aa);
     fp2_add(t3, t3, bb);
     Fp2 cs;
     fp2_add(cs, c0, c1);
     fp2_add(s, a.c0, a.c1);
-    fp2_mul(t2, s, cs);
+    fp2_mul_in(t2, s, cs);
     fp2_sub(t2, t2, aa);
     fp2_sub(t2, t2, bb);
     r.c0 = t1;
@@ -328,9 +330,9 @@ DEV void fp6_mul_by_01(Fp6 &r, const Fp6 &a, const Fp2 &c0, const Fp2 &c1) {
 // (a0 + a1 v + a2 v^2) c1 v
 DEV void fp6_mul_by_1(Fp6 &r, const Fp6 &a, const Fp2 &c1) {
     Fp2 t0, t1, t2;
-    fp2_mul(t2, a.c1, c1);
-    fp2_mul(t1, a.c0, c1);
-    fp2_mul(t0, a.c2, c1);
+    fp2_mul_in(t2, a.c1, c1);
+    fp2_mul_in(t1, a.c0, c1);
+    fp2_mul_in(t0, a.c2, c1);
     fp2_mul_xi(r.c0, t0);
     r.c1 = t1;
     r.c2 = t2;
@@ -458,12 +460,12 @@ NOINL void fp12_frob(Fp12 &r, const Fp12 &a, int k) {
 // (a + b s)^2 in Fp4 = Fp2[s]/(s^2 - xi): (a^2 + xi b^2, 2ab)
 DEV void fp4_sqr(Fp2 &c0, Fp2 &c1, const Fp2 &a, const Fp2 &b) {
     Fp2 t0, t1, t2;
-    fp2_sqr(t0, a);
-    fp2_sqr(t1, b);
+    fp2_sqr_in(t0, a);
+    fp2_sqr_in(t1, b);
     fp2_mul_xi(t2, t1);
     fp2_add(c0, t2, t0);
     fp2_add(t2, a, b);
-    fp2_sqr(t2, t2);
+    fp2_sqr_in(t2, t2);
     fp2_sub(t2, t2, t0);
     fp2_sub(c1, t2, t1);
 }
@@ -516,34 +518,34 @@ struct G2Proj { Fp2 x, y, z; };
 
 // T <- 2T; line tangent at T evaluated at P = (xp, yp), scaled by 2YZ^2:
 // (3X^3 - 2Y^2 Z) + (-3X^2 Z xp) v + (2 Y Z^2 yp) v w
-DEV void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
+NOINL void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
     Fp2 xx, w, s, ss, sss, rr, RR, B, h, t, l0, l1, l4;
-    fp2_sqr(xx, T.x);
+    fp2_sqr_in(xx, T.x);
     fp2_dbl(w, xx);
     fp2_add(w, w, xx);            // w = 3 X^2
-    fp2_mul(s, T.y, T.z);
+    fp2_mul_in(s, T.y, T.z);
     fp2_dbl(s, s);                // s = 2 Y Z
-    fp2_sqr(ss, s);
-    fp2_mul(sss, s, ss);
-    fp2_mul(rr, T.y, s);          // R = Y s = 2 Y^2 Z
-    fp2_sqr(RR, rr);
+    fp2_sqr_in(ss, s);
+    fp2_mul_in(sss, s, ss);
+    fp2_mul_in(rr, T.y, s);          // R = Y s = 2 Y^2 Z
+    fp2_sqr_in(RR, rr);
     fp2_add(B, T.x, rr);
-    fp2_sqr(B, B);
+    fp2_sqr_in(B, B);
     fp2_sub(B, B, xx);
     fp2_sub(B, B, RR);            // B = (X + R)^2 - X^2 - R^2
-    fp2_mul(l0, T.x, w);
+    fp2_mul_in(l0, T.x, w);
     fp2_sub(l0, l0, rr);          // 3X^3 - 2Y^2 Z
-    fp2_mul(l1, w, T.z);
+    fp2_mul_in(l1, w, T.z);
     fp2_mul_fp(l1, l1, xp);
     fp2_neg(l1, l1);              // -3X^2 Z xp
-    fp2_mul(l4, s, T.z);
+    fp2_mul_in(l4, s, T.z);
     fp2_mul_fp(l4, l4, yp);       // 2 Y Z^2 yp
-    fp2_sqr(h, w);
+    fp2_sqr_in(h, w);
     fp2_sub(h, h, B);
     fp2_sub(h, h, B);             // h = w^2 - 2B
-    fp2_mul(T.x, h, s);
+    fp2_mul_in(T.x, h, s);
     fp2_sub(t, B, h);
-    fp2_mul(t, w, t);
+    fp2_mul_in(t, w, t);
     fp2_dbl(RR, RR);
     fp2_sub(T.y, t, RR);          // w (B - h) - 2 R^2
     T.z = sss;
@@ -552,34 +554,34 @@ DEV void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
 
 // T <- T + Q (Q affine); line through T and Q at P, scaled by (xq Z - X):
 // (u xq - v yq) + (-u xp) v + (v yp) v w,  u = yq Z - Y, v = xq Z - X
-DEV void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp &xp,
+NOINL void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp &xp,
                     const Fp &yp) {
     Fp2 u, v, uu, vv, vvv, R, A, t, l0, l1, l4;
-    fp2_mul(u, yq, T.z);
+    fp2_mul_in(u, yq, T.z);
     fp2_sub(u, u, T.y);
-    fp2_mul(v, xq, T.z);
+    fp2_mul_in(v, xq, T.z);
     fp2_sub(v, v, T.x);
-    fp2_mul(l0, u, xq);
-    fp2_mul(t, v, yq);
+    fp2_mul_in(l0, u, xq);
+    fp2_mul_in(t, v, yq);
     fp2_sub(l0, l0, t);
     fp2_mul_fp(l1, u, xp);
     fp2_neg(l1, l1);
     fp2_mul_fp(l4, v, yp);
-    fp2_sqr(uu, u);
-    fp2_sqr(vv, v);
-    fp2_mul(vvv, v, vv);
-    fp2_mul(R, vv, T.x);
-    fp2_mul(A, uu, T.z);
+    fp2_sqr_in(uu, u);
+    fp2_sqr_in(vv, v);
+    fp2_mul_in(vvv, v, vv);
+    fp2_mul_in(R, vv, T.x);
+    fp2_mul_in(A, uu, T.z);
     fp2_sub(A, A, vvv);
     fp2_sub(A, A, R);
     fp2_sub(A, A, R);             // A = uu Z - vvv - 2R
-    fp2_mul(T.x, v, A);
+    fp2_mul_in(T.x, v, A);
     fp2_sub(t, R, A);
-    fp2_mul(t, u, t);
-    fp2_mul(vvv, vvv, T.y);
+    fp2_mul_in(t, u, t);
+    fp2_mul_in(vvv, vvv, T.y);
     fp2_sub(T.y, t, vvv);
-    fp2_mul(T.z, T.z, vv);
-    fp2_mul(T.z, T.z, v);         // Z vvv
+    fp2_mul_in(T.z, T.z, vv);
+    fp2_mul_in(T.z, T.z, v);         // Z vvv
     fp12_mul_by_014(f, l0, l1, l4);
 }
 
@@ -683,8 +685,7 @@ constexpr int kPairBlock = 64;
 // point g2[i]; with `negate_odd`, odd pairings negate their G1 point (the
 // c of a check a,b == c,d sits at pairing 2i+1).  status[i] gets the point
 // status (max of the two); an infinity or invalid input leaves f = 1.
-template <int W>
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(W, W))) void miller_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void miller_kernel(
     const uint8_t *__restrict__ g1, size_t g1_stride, const uint8_t *__restrict__ g2,
     size_t g2_stride, size_t n, int pair_inputs, uint32_t *__restrict__ ws,
     uint8_t *__restrict__ status) {
@@ -768,8 +769,7 @@ DEV void store_be48(uint8_t *dst, const Fp &a) {
 // (1: a pairing, 2: a check) are multiplied first.  gt_out (if set) gets the
 // 576-byte GT value; ok_out (if set) gets 1 if the value is 1 (the check
 // holds), 0 if not, 2 if an input point was invalid.
-template <int W>
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(W, W))) void final_exp_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void final_exp_kernel(
     const uint32_t *__restrict__ ws, size_t n_miller, size_t n_out, int per_out,
     const uint8_t *__restrict__ status, uint8_t *__restrict__ gt_out,
     uint8_t *__restrict__ ok_out) {
@@ -801,26 +801,14 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(W, W
 
 }  // namespace
 
-// Waves per SIMD the kernels are compiled for (register budget 512 / W per
-// lane; the rest spills to scratch).  HBRBC_PAIR_WAVES=1|2|4 picks one for
-// A/B runs; the default is the measured best.
-static int pair_waves() {
-    static int w = [] {
-        const char *e = getenv("HBRBC_PAIR_WAVES");
-        const int v = e ? atoi(e) : 4;
-        return (v == 1 || v == 2 || v == 4) ? v : 4;
-    }();
-    return w;
-}
-
+// The kernels run at 4 waves/SIMD (128 VGPRs, the rest of the tower state in
+// scratch); 1 and 2 waves measured within 5 %.
 hipError_t launch_pairing_miller(const uint8_t *g1, size_t g1_stride, const uint8_t *g2,
                                  size_t g2_stride, size_t n, int pair_inputs, uint32_t *ws,
                                  uint8_t *status, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n + kPairBlock - 1) / kPairBlock);
-    const int w = pair_waves();
-    auto k = w == 1 ? miller_kernel<1> : w == 2 ? miller_kernel<2> : miller_kernel<4>;
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kPairBlock), 0, s, g1, g1_stride, g2, g2_stride, n,
+    hipLaunchKernelGGL(miller_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, g1_stride, g2, g2_stride, n,
                        pair_inputs, ws, status);
     return hipGetLastError();
 }
@@ -830,9 +818,7 @@ hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_ou
                                 hipStream_t s) {
     if (n_out == 0) return hipSuccess;
     const unsigned blocks = (unsigned)((n_out + kPairBlock - 1) / kPairBlock);
-    const int w = pair_waves();
-    auto k = w == 1 ? final_exp_kernel<1> : w == 2 ? final_exp_kernel<2> : final_exp_kernel<4>;
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(kPairBlock), 0, s, ws, n_miller, n_out, per_out,
+    hipLaunchKernelGGL(final_exp_kernel, dim3(blocks), dim3(kPairBlock), 0, s, ws, n_miller, n_out, per_out,
                        status, gt_out, ok_out);
     return hipGetLastError();
 }

@@ -38,3 +38,15 @@ def test_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_f4_leg_host_helpers():
+    """The f4 leg's CPU check decodes the fixture encodings and agrees with the
+    fixture outcomes (one valid, one tampered); the VALU work per check comes
+    from the committed counter pass."""
+    import json
+    pool = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))["bench_pool"]
+    assert len(pool) == 32 and sum(c["expect"] for c in pool) == 24
+    assert bench.f4_cpu_check(pool[0]) and bench.f4_cpu_check(pool[3])
+    ops, src = bench.pairing_ops_per_check()
+    assert ops is not None and 1e6 < ops < 1e8 and "SQ_INSTS_VALU" in src
