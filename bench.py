@@ -164,7 +164,7 @@ def gen_present(torch, seed, first, count, n, n_erase, dev):
 
 # --------------------------------------------------------------- accounting --
 def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase, elapsed,
-                config):
+                config, unframe_fused=False):
     """Roofline of the dominant kernel from live per-stage HIP-event times.
     Sponge kernels are VALU-bound (Keccak-f[1600]); the HBM view is reported
     beside it."""
@@ -179,8 +179,10 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
         "proofs": n * dslots * 32 * 2 + n,
         "validate": n * (S + 32 * (dslots + 1) + 1),
         "decode_matrix": n + m * k,
-        "reconstruct": (k + n_erase) * S,
-        "unframe": k * S + plen,
+        # fused unframe: the reconstruct kernel also writes the payload; the
+        # unframe stage is then decode_check + the zero-fill past the length
+        "reconstruct": (k + n_erase) * S + (plen if unframe_fused else 0),
+        "unframe": (32 + max(0, k * S - 4 - plen)) if unframe_fused else k * S + plen,
     }.items()}
     perms = {"leaf_hash": per_launch * n * L, "validate": per_launch * (n * L + n * dslots),
              "tree_levels": per_launch * (n - 1)}
@@ -423,7 +425,9 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
             stages[st_name] = (a0 + ms, c0 + cnt)
     value = float(count) * plen * world * args.steps / elapsed / 1e9
     roof = roofline_of(stages, args.steps, count / nsub, n, k, m, S, plen, rb.node_count,
-                       rb.dslots, n_erase, elapsed, args.config)
+                       rb.dslots, n_erase, elapsed, args.config,
+                       unframe_fused=rb.unframe_fused(S, out.stride(0)))
+    roof["unframe_fused"] = rb.unframe_fused(S, out.stride(0))
     return {
         "value": value, "ms_per_step": elapsed / args.steps * 1e3, "roofline": roof,
         "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},

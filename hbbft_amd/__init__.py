@@ -128,6 +128,7 @@ def lib():
         "hbrbc_jit_decode_groups": (_S, [_S, _S, _P]),
         "hbrbc_jit_build_decode": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p]),
         "hbrbc_jit_decode_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p, _S]),
+        "hbrbc_unframe_fused": (ctypes.c_int, [_P, _S, _S, _S]),
         "hbrbc_pairing_workspace_size": (_S, [_S]),
         "hbrbc_pairing_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P, _P]),
         "hbrbc_pairing_check_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P]),
@@ -665,6 +666,12 @@ class RbcBatch:
         _check(lib().hbrbc_reconstruct_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
                                              slab.stride(0), _ptr(present), slab.shape[0],
                                              _ptr(status), self._stream(stream)))
+
+    def unframe_fused(self, S, payload_stride, rows_per_block=0):
+        """Whether decode writes the payload from the reconstruct kernel (same
+        outputs either way; where the bytes move, for accounting)."""
+        return bool(lib().hbrbc_unframe_fused(self.coding.handle, S, payload_stride,
+                                              rows_per_block))
 
     def decode(self, slab, S, present, roots, nodes, payload_out, plen_out, status,
                stream=None):

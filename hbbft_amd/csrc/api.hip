@@ -1883,6 +1883,16 @@ const char *hbrbc_stage_name(int stage) {
     return (stage >= 0 && stage < HBRBC_STAGE_COUNT) ? names[stage] : "?";
 }
 
+int hbrbc_unframe_fused(const hbrbc_ctx *c, size_t shard_len, size_t payload_stride,
+                        size_t rows_per_block) {
+    if (!c) return 0;
+    RowMap rows = plain_rows(round_up(shard_len, 16));
+    if (rows_per_block && rows_per_block < c->n) rows.rb = (uint32_t)rows_per_block;
+    const auto ds = c->dec_spec.find(code_rb(rows));
+    const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
+    return unframe_fusable(c, shard_len, payload_stride) && !spec ? 1 : 0;
+}
+
 // ---- threshold-decrypt share verification (pairing.hip) ----
 size_t hbrbc_pairing_workspace_size(size_t pairings) {
     return round_up(pairings * 576, 256) + round_up(pairings, 256);
