@@ -568,6 +568,7 @@ def pairing_ops_per_check():
 
 
 def f4_cpu_check(item):
+    """One fixture check through the pure-Python restatement (tests use it)."""
     from oracle import bls_oracle as B
     a, b, c, d = (bytes.fromhex(item[k]) for k in "abcd")
 
@@ -582,36 +583,42 @@ def f4_cpu_check(item):
     return B.pairing_check(g1(a), g2(b), g1(c), g2(d)) == item["expect"]
 
 
-def f4_cpu_baseline(pool, reps):
-    """oracle/bls_oracle.py (pure-Python restatement of the pairing crate) on the
-    cgroup's cores (spawned worker processes) and on one core; median of reps."""
-    import multiprocessing as mp
+def f4_cpu_baseline(pool, reps, target_s=2.0):
+    """oracle/bls_pairing.c (C restatement of the pairing crate: 6 x 64-bit
+    Montgomery limbs, Karatsuba tower, sparse lines, the crate's final
+    exponentiation) on the cgroup's cores and on one core, over the fixture
+    pool tiled, median of reps; outcomes checked against the fixtures."""
+    from oracle import bls_c
     cpus = len(os.sched_getaffinity(0))
     quota = cpu_quota()
-    procs = max(1, min(cpus, int(quota)) if quota else cpus)
-    items = [pool[i % len(pool)] for i in range(24 * procs)]   # ~3 s per rep
-    times = []
-    with mp.get_context("spawn").Pool(procs) as p:
-        p.map(f4_cpu_check, items[:procs])                      # warm-up / import
+    threads = max(1, min(cpus, int(quota)) if quota else cpus)
+    g1 = b"".join(bytes.fromhex(c["a"]) + bytes.fromhex(c["c"]) for c in pool)
+    g2 = b"".join(bytes.fromhex(c["b"]) + bytes.fromhex(c["d"]) for c in pool)
+    want = bytes(1 if c["expect"] else 0 for c in pool)
+
+    def measure(th):
+        t0 = time.perf_counter()
+        ok = bls_c.check_batch(g1, g2, len(pool), th)        # calibration + outcome check
+        per = (time.perf_counter() - t0) / len(pool)
+        assert ok == want, "C restatement disagrees with the fixture outcomes"
+        tiles = max(1, int(target_s / per / len(pool)))
+        times = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            ok = p.map(f4_cpu_check, items)
+            ok = bls_c.check_batch(g1 * tiles, g2 * tiles, len(pool) * tiles, th)
             times.append(time.perf_counter() - t0)
-            assert all(ok), "CPU restatement disagrees with the fixture outcomes"
-    times.sort()
-    t1 = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        assert f4_cpu_check(pool[0])
-        t1.append(time.perf_counter() - t0)
-    t1.sort()
-    med, med1 = times[len(times) // 2], t1[len(t1) // 2]
-    return {"value": len(items) / med, "unit": "checks/s", "cores": procs, "kind": "port",
-            "reps": reps, "single_core": {"value": 1.0 / med1, "unit": "checks/s", "cores": 1},
-            "sample": "%d checks (the fixture pool) through oracle/bls_oracle.py, a pure-Python "
-                      "big-integer restatement of the pairing crate (far slower than the Rust "
-                      "crate, which cannot be built here), %d worker processes; median of %d "
-                      "reps %.2f s" % (len(items), procs, reps, med)}
+            assert ok == want * tiles
+        times.sort()
+        return len(pool) * tiles, times[len(times) // 2]
+
+    n, med = measure(threads)
+    n1, med1 = measure(1)
+    return {"value": n / med, "unit": "checks/s", "cores": threads, "kind": "port",
+            "reps": reps, "single_core": {"value": n1 / med1, "unit": "checks/s", "cores": 1,
+                                          "sample": "%d checks, median of %d" % (n1, reps)},
+            "sample": "%d checks (the 32-check fixture pool tiled) through oracle/bls_pairing.c, "
+                      "a C restatement of the pairing crate (the Rust crate cannot be built "
+                      "here), %d threads; median of %d reps %.2f s" % (n, threads, reps, med)}
 
 
 def run_threshold(args, rank, world, dev):

@@ -1,0 +1,663 @@
+/* bls_pairing.c -- CPU restatement of the BLS12-381 pairing check behind
+ * threshold-decrypt share verification, in C for a credible
+ * CPU baseline (bench.py's f4 cpu_baseline leg).
+ *
+ * TEST INFRASTRUCTURE ONLY (like rbc_oracle.c): loaded by tests/ and by the
+ * bench's cpu_baseline leg, never by the product path.  Pinned against
+ * oracle/bls_oracle.py (the plain-math restatement) through the golden GT
+ * bytes of tests/golden/bls_vectors.json (tests/test_bls_oracle.py).
+ *
+ * What it restates: `threshold_crypto` (rev 624eeee, Cargo.toml:36) checks
+ *   e(share, H) == e(pk_i, W)      (verify_decryption_share,
+ *                                   /root/reference/src/threshold_decrypt.rs:220-228)
+ *   e(G1::one(), W) == e(U, H)     (Ciphertext::verify, threshold_decrypt.rs:142)
+ * with `pairing`'s BLS12-381 (not vendored): Fp 381-bit Montgomery on 6 x
+ * 64-bit limbs (the crate's own limb layout), Fp2 = Fp[u]/(u^2+1), Fp6 =
+ * Fp2[v]/(v^3-(u+1)), Fp12 = Fp6[w]/(w^2-v); Miller loop over |x| =
+ * 0xd201000000010000 with projective doubling/addition on the twist and
+ * sparse (c0, c1, c4) lines, conjugated (x < 0); final exponentiation = easy
+ * part + the crate's hard-part chain.  Scalar code, one check per thread.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+typedef struct { uint64_t l[6]; } fp;
+typedef struct { fp c0, c1; } fp2;
+typedef struct { fp2 c0, c1, c2; } fp6;
+typedef struct { fp6 c0, c1; } fp12;
+
+static const uint64_t P[6] = {0xb9feffffffffaaabull, 0x1eabfffeb153ffffull, 0x6730d2a0f6b0f624ull,
+                              0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
+static const uint64_t XABS = 0xd201000000010000ull;
+static uint64_t INV;                       /* -p^-1 mod 2^64 */
+static fp R2, ONE, B1;                     /* R^2, R, 4R (mod p) */
+static fp2 F6C1[4], F6C2[4], F12C1[4];     /* Frobenius coefficients */
+static int inited;
+
+/* ---------------------------------------------------------------- Fp */
+static int geq_p(const uint64_t *a) {
+    for (int i = 5; i >= 0; --i) {
+        if (a[i] != P[i]) return a[i] > P[i];
+    }
+    return 1;
+}
+static void sub_p(uint64_t *a) {
+    u128 br = 0;
+    for (int i = 0; i < 6; ++i) {
+        u128 d = (u128)a[i] - P[i] - br;
+        a[i] = (uint64_t)d;
+        br = (d >> 64) & 1;
+    }
+}
+static void fp_add(fp *r, const fp *a, const fp *b) {
+    u128 c = 0;
+    for (int i = 0; i < 6; ++i) {
+        c += (u128)a->l[i] + b->l[i];
+        r->l[i] = (uint64_t)c;
+        c >>= 64;
+    }
+    if (geq_p(r->l)) sub_p(r->l);
+}
+static void fp_sub(fp *r, const fp *a, const fp *b) {
+    u128 br = 0;
+    uint64_t t[6];
+    for (int i = 0; i < 6; ++i) {
+        u128 d = (u128)a->l[i] - b->l[i] - br;
+        t[i] = (uint64_t)d;
+        br = (d >> 64) & 1;
+    }
+    if (br) {
+        u128 c = 0;
+        for (int i = 0; i < 6; ++i) {
+            c += (u128)t[i] + P[i];
+            t[i] = (uint64_t)c;
+            c >>= 64;
+        }
+    }
+    memcpy(r->l, t, sizeof t);
+}
+static void fp_neg(fp *r, const fp *a) {
+    fp z;
+    memset(&z, 0, sizeof z);
+    fp_sub(r, &z, a);
+}
+static void fp_mul(fp *r, const fp *a, const fp *b) {     /* CIOS */
+    uint64_t t[8] = {0};
+    for (int i = 0; i < 6; ++i) {
+        u128 c = 0;
+        for (int j = 0; j < 6; ++j) {
+            c = (u128)a->l[j] * b->l[i] + t[j] + (c >> 64);
+            t[j] = (uint64_t)c;
+        }
+        c = (u128)t[6] + (c >> 64);
+        t[6] = (uint64_t)c;
+        t[7] = (uint64_t)(c >> 64);
+        uint64_t m = t[0] * INV;
+        c = (u128)m * P[0] + t[0];
+        for (int j = 1; j < 6; ++j) {
+            c = (u128)m * P[j] + t[j] + (c >> 64);
+            t[j - 1] = (uint64_t)c;
+        }
+        c = (u128)t[6] + (c >> 64);
+        t[5] = (uint64_t)c;
+        t[6] = t[7] + (uint64_t)(c >> 64);
+    }
+    if (t[6] || geq_p(t)) sub_p(t);
+    memcpy(r->l, t, 48);
+}
+static int fp_eq(const fp *a, const fp *b) { return memcmp(a, b, sizeof *a) == 0; }
+/* a^e, e given as little-endian 64-bit limbs */
+static void fp_pow(fp *r, const fp *a, const uint64_t *e, int n) {
+    fp acc = ONE, base = *a;
+    for (int w = 0; w < n; ++w)
+        for (int b = 0; b < 64; ++b) {
+            if ((e[w] >> b) & 1) fp_mul(&acc, &acc, &base);
+            fp_mul(&base, &base, &base);
+        }
+    *r = acc;
+}
+static void fp_inv(fp *r, const fp *a) {
+    uint64_t e[6];
+    memcpy(e, P, sizeof e);
+    e[0] -= 2;
+    fp_pow(r, a, e, 6);
+}
+
+/* ---------------------------------------------------------------- Fp2 */
+static void f2_add(fp2 *r, const fp2 *a, const fp2 *b) { fp_add(&r->c0, &a->c0, &b->c0); fp_add(&r->c1, &a->c1, &b->c1); }
+static void f2_sub(fp2 *r, const fp2 *a, const fp2 *b) { fp_sub(&r->c0, &a->c0, &b->c0); fp_sub(&r->c1, &a->c1, &b->c1); }
+static void f2_neg(fp2 *r, const fp2 *a) { fp_neg(&r->c0, &a->c0); fp_neg(&r->c1, &a->c1); }
+static void f2_dbl(fp2 *r, const fp2 *a) { f2_add(r, a, a); }
+static void f2_mul(fp2 *r, const fp2 *a, const fp2 *b) {
+    fp t0, t1, s0, s1;
+    fp_mul(&t0, &a->c0, &b->c0);
+    fp_mul(&t1, &a->c1, &b->c1);
+    fp_add(&s0, &a->c0, &a->c1);
+    fp_add(&s1, &b->c0, &b->c1);
+    fp_mul(&s0, &s0, &s1);
+    fp_sub(&r->c0, &t0, &t1);
+    fp_sub(&s0, &s0, &t0);
+    fp_sub(&r->c1, &s0, &t1);
+}
+static void f2_sqr(fp2 *r, const fp2 *a) { f2_mul(r, a, a); }
+static void f2_mul_fp(fp2 *r, const fp2 *a, const fp *s) { fp_mul(&r->c0, &a->c0, s); fp_mul(&r->c1, &a->c1, s); }
+static void f2_mul_xi(fp2 *r, const fp2 *a) {   /* * (u + 1) */
+    fp t0, t1;
+    fp_sub(&t0, &a->c0, &a->c1);
+    fp_add(&t1, &a->c0, &a->c1);
+    r->c0 = t0;
+    r->c1 = t1;
+}
+static void f2_conj(fp2 *r, const fp2 *a) { r->c0 = a->c0; fp_neg(&r->c1, &a->c1); }
+static void f2_inv(fp2 *r, const fp2 *a) {
+    fp n0, n1;
+    fp_mul(&n0, &a->c0, &a->c0);
+    fp_mul(&n1, &a->c1, &a->c1);
+    fp_add(&n0, &n0, &n1);
+    fp_inv(&n0, &n0);
+    fp_mul(&r->c0, &a->c0, &n0);
+    fp_mul(&n1, &a->c1, &n0);
+    fp_neg(&r->c1, &n1);
+}
+static void f2_pow(fp2 *r, const fp2 *a, const uint64_t *e, int n) {
+    fp2 acc, base = *a;
+    acc.c0 = ONE;
+    memset(&acc.c1, 0, sizeof(fp));
+    for (int w = 0; w < n; ++w)
+        for (int b = 0; b < 64; ++b) {
+            if ((e[w] >> b) & 1) f2_mul(&acc, &acc, &base);
+            f2_mul(&base, &base, &base);
+        }
+    *r = acc;
+}
+
+/* ---------------------------------------------------------------- Fp6 / Fp12 */
+static void f6_add(fp6 *r, const fp6 *a, const fp6 *b) { f2_add(&r->c0, &a->c0, &b->c0); f2_add(&r->c1, &a->c1, &b->c1); f2_add(&r->c2, &a->c2, &b->c2); }
+static void f6_sub(fp6 *r, const fp6 *a, const fp6 *b) { f2_sub(&r->c0, &a->c0, &b->c0); f2_sub(&r->c1, &a->c1, &b->c1); f2_sub(&r->c2, &a->c2, &b->c2); }
+static void f6_neg(fp6 *r, const fp6 *a) { f2_neg(&r->c0, &a->c0); f2_neg(&r->c1, &a->c1); f2_neg(&r->c2, &a->c2); }
+static void f6_mul_v(fp6 *r, const fp6 *a) {     /* (a0, a1, a2) v = (xi a2, a0, a1) */
+    fp2 t;
+    f2_mul_xi(&t, &a->c2);
+    r->c2 = a->c1;
+    r->c1 = a->c0;
+    r->c0 = t;
+}
+static void f6_mul(fp6 *r, const fp6 *a, const fp6 *b) {   /* Karatsuba, as the crate */
+    fp2 aa, bb, cc, s, t, t1, t2, t3;
+    f2_mul(&aa, &a->c0, &b->c0);
+    f2_mul(&bb, &a->c1, &b->c1);
+    f2_mul(&cc, &a->c2, &b->c2);
+    f2_add(&s, &a->c1, &a->c2);
+    f2_add(&t, &b->c1, &b->c2);
+    f2_mul(&t1, &s, &t);
+    f2_sub(&t1, &t1, &bb);
+    f2_sub(&t1, &t1, &cc);
+    f2_mul_xi(&t1, &t1);
+    f2_add(&t1, &t1, &aa);
+    f2_add(&s, &a->c0, &a->c2);
+    f2_add(&t, &b->c0, &b->c2);
+    f2_mul(&t3, &s, &t);
+    f2_sub(&t3, &t3, &aa);
+    f2_add(&t3, &t3, &bb);
+    f2_sub(&t3, &t3, &cc);
+    f2_add(&s, &a->c0, &a->c1);
+    f2_add(&t, &b->c0, &b->c1);
+    f2_mul(&t2, &s, &t);
+    f2_sub(&t2, &t2, &aa);
+    f2_sub(&t2, &t2, &bb);
+    f2_mul_xi(&cc, &cc);
+    f2_add(&t2, &t2, &cc);
+    r->c0 = t1;
+    r->c1 = t2;
+    r->c2 = t3;
+}
+/* (a0 + a1 v + a2 v^2)(c0 + c1 v) and (...) c1 v: the sparse products */
+static void f6_mul_by_01(fp6 *r, const fp6 *a, const fp2 *c0, const fp2 *c1) {
+    fp2 aa, bb, s, t1, t2, t3, cs;
+    f2_mul(&aa, &a->c0, c0);
+    f2_mul(&bb, &a->c1, c1);
+    f2_add(&s, &a->c1, &a->c2);
+    f2_mul(&t1, &s, c1);
+    f2_sub(&t1, &t1, &bb);
+    f2_mul_xi(&t1, &t1);
+    f2_add(&t1, &t1, &aa);
+    f2_add(&s, &a->c0, &a->c2);
+    f2_mul(&t3, &s, c0);
+    f2_sub(&t3, &t3, &aa);
+    f2_add(&t3, &t3, &bb);
+    f2_add(&cs, c0, c1);
+    f2_add(&s, &a->c0, &a->c1);
+    f2_mul(&t2, &s, &cs);
+    f2_sub(&t2, &t2, &aa);
+    f2_sub(&t2, &t2, &bb);
+    r->c0 = t1;
+    r->c1 = t2;
+    r->c2 = t3;
+}
+static void f6_mul_by_1(fp6 *r, const fp6 *a, const fp2 *c1) {
+    fp2 t0, t1, t2;
+    f2_mul(&t2, &a->c1, c1);
+    f2_mul(&t1, &a->c0, c1);
+    f2_mul(&t0, &a->c2, c1);
+    f2_mul_xi(&r->c0, &t0);
+    r->c1 = t1;
+    r->c2 = t2;
+}
+static void f6_inv(fp6 *r, const fp6 *a) {
+    fp2 c0, c1, c2, t, u;
+    f2_sqr(&c0, &a->c0);
+    f2_mul(&t, &a->c1, &a->c2);
+    f2_mul_xi(&t, &t);
+    f2_sub(&c0, &c0, &t);
+    f2_sqr(&c1, &a->c2);
+    f2_mul_xi(&c1, &c1);
+    f2_mul(&t, &a->c0, &a->c1);
+    f2_sub(&c1, &c1, &t);
+    f2_sqr(&c2, &a->c1);
+    f2_mul(&t, &a->c0, &a->c2);
+    f2_sub(&c2, &c2, &t);
+    f2_mul(&t, &a->c2, &c1);
+    f2_mul(&u, &a->c1, &c2);
+    f2_add(&t, &t, &u);
+    f2_mul_xi(&t, &t);
+    f2_mul(&u, &a->c0, &c0);
+    f2_add(&t, &t, &u);
+    f2_inv(&t, &t);
+    f2_mul(&r->c0, &c0, &t);
+    f2_mul(&r->c1, &c1, &t);
+    f2_mul(&r->c2, &c2, &t);
+}
+static void f12_mul(fp12 *r, const fp12 *a, const fp12 *b) {
+    fp6 aa, bb, s, t;
+    f6_mul(&aa, &a->c0, &b->c0);
+    f6_mul(&bb, &a->c1, &b->c1);
+    f6_add(&s, &a->c0, &a->c1);
+    f6_add(&t, &b->c0, &b->c1);
+    f6_mul(&s, &s, &t);
+    f6_sub(&s, &s, &aa);
+    f6_sub(&r->c1, &s, &bb);
+    f6_mul_v(&bb, &bb);
+    f6_add(&r->c0, &aa, &bb);
+}
+static void f12_sqr(fp12 *r, const fp12 *a) {
+    fp6 ab, s, t;
+    f6_mul(&ab, &a->c0, &a->c1);
+    f6_add(&s, &a->c0, &a->c1);
+    f6_mul_v(&t, &a->c1);
+    f6_add(&t, &t, &a->c0);
+    f6_mul(&s, &s, &t);
+    f6_sub(&s, &s, &ab);
+    f6_mul_v(&t, &ab);
+    f6_sub(&r->c0, &s, &t);
+    f6_add(&r->c1, &ab, &ab);
+}
+static void f12_conj(fp12 *r, const fp12 *a) { r->c0 = a->c0; f6_neg(&r->c1, &a->c1); }
+static void f12_inv(fp12 *r, const fp12 *a) {
+    fp6 t0, t1;
+    f6_mul(&t0, &a->c0, &a->c0);
+    f6_mul(&t1, &a->c1, &a->c1);
+    f6_mul_v(&t1, &t1);
+    f6_sub(&t0, &t0, &t1);
+    f6_inv(&t0, &t0);
+    f6_mul(&r->c0, &a->c0, &t0);
+    f6_mul(&t1, &a->c1, &t0);
+    f6_neg(&r->c1, &t1);
+}
+static void f12_frob(fp12 *r, const fp12 *a, int k) {
+    fp6 c0 = a->c0, c1 = a->c1;
+    fp2 *x[6] = {&c0.c0, &c0.c1, &c0.c2, &c1.c0, &c1.c1, &c1.c2};
+    if (k & 1)
+        for (int i = 0; i < 6; ++i) f2_conj(x[i], x[i]);
+    f2_mul(&c0.c1, &c0.c1, &F6C1[k]);
+    f2_mul(&c0.c2, &c0.c2, &F6C2[k]);
+    f2_mul(&c1.c1, &c1.c1, &F6C1[k]);
+    f2_mul(&c1.c2, &c1.c2, &F6C2[k]);
+    for (int i = 3; i < 6; ++i) f2_mul(x[i], x[i], &F12C1[k]);
+    r->c0 = c0;
+    r->c1 = c1;
+}
+static void f12_one(fp12 *r) {
+    memset(r, 0, sizeof *r);
+    r->c0.c0.c0 = ONE;
+}
+static int f12_is_one(const fp12 *a) {
+    fp12 one;
+    f12_one(&one);
+    return memcmp(a, &one, sizeof one) == 0;
+}
+static void f12_exp_by_x(fp12 *r, const fp12 *a, int shift) {
+    const uint64_t e = XABS >> shift;
+    fp12 acc = *a;
+    for (int b = 62 - shift; b >= 0; --b) {
+        f12_sqr(&acc, &acc);
+        if ((e >> b) & 1) f12_mul(&acc, &acc, a);
+    }
+    f12_conj(r, &acc);
+}
+
+/* ---------------------------------------------------------------- pairing */
+/* f * (l0 + l1 v + l4 v w): the crate's mul_by_014 */
+static void mul_line(fp12 *f, const fp2 *l0, const fp2 *l1, const fp2 *l4) {
+    fp6 aa, bb, s;
+    fp2 o;
+    f6_mul_by_01(&aa, &f->c0, l0, l1);
+    f6_mul_by_1(&bb, &f->c1, l4);
+    f2_add(&o, l1, l4);
+    f6_add(&s, &f->c1, &f->c0);
+    f6_mul_by_01(&s, &s, l0, &o);
+    f6_sub(&s, &s, &aa);
+    f6_sub(&f->c1, &s, &bb);
+    f6_mul_v(&bb, &bb);
+    f6_add(&f->c0, &bb, &aa);
+}
+typedef struct { fp2 x, y, z; } g2p;
+static void dbl_step(g2p *T, fp12 *f, const fp *xp, const fp *yp) {
+    fp2 xx, w, s, ss, sss, rr, RR, B, h, t, l0, l1, l4;
+    f2_sqr(&xx, &T->x);
+    f2_dbl(&w, &xx);
+    f2_add(&w, &w, &xx);
+    f2_mul(&s, &T->y, &T->z);
+    f2_dbl(&s, &s);
+    f2_sqr(&ss, &s);
+    f2_mul(&sss, &s, &ss);
+    f2_mul(&rr, &T->y, &s);
+    f2_sqr(&RR, &rr);
+    f2_add(&B, &T->x, &rr);
+    f2_sqr(&B, &B);
+    f2_sub(&B, &B, &xx);
+    f2_sub(&B, &B, &RR);
+    f2_mul(&l0, &T->x, &w);
+    f2_sub(&l0, &l0, &rr);
+    f2_mul(&l1, &w, &T->z);
+    f2_mul_fp(&l1, &l1, xp);
+    f2_neg(&l1, &l1);
+    f2_mul(&l4, &s, &T->z);
+    f2_mul_fp(&l4, &l4, yp);
+    f2_sqr(&h, &w);
+    f2_sub(&h, &h, &B);
+    f2_sub(&h, &h, &B);
+    f2_mul(&T->x, &h, &s);
+    f2_sub(&t, &B, &h);
+    f2_mul(&t, &w, &t);
+    f2_dbl(&RR, &RR);
+    f2_sub(&T->y, &t, &RR);
+    T->z = sss;
+    mul_line(f, &l0, &l1, &l4);
+}
+static void add_step(g2p *T, fp12 *f, const fp2 *xq, const fp2 *yq, const fp *xp, const fp *yp) {
+    fp2 u, v, uu, vv, vvv, R, A, t, l0, l1, l4;
+    f2_mul(&u, yq, &T->z);
+    f2_sub(&u, &u, &T->y);
+    f2_mul(&v, xq, &T->z);
+    f2_sub(&v, &v, &T->x);
+    f2_mul(&l0, &u, xq);
+    f2_mul(&t, &v, yq);
+    f2_sub(&l0, &l0, &t);
+    f2_mul_fp(&l1, &u, xp);
+    f2_neg(&l1, &l1);
+    f2_mul_fp(&l4, &v, yp);
+    f2_sqr(&uu, &u);
+    f2_sqr(&vv, &v);
+    f2_mul(&vvv, &v, &vv);
+    f2_mul(&R, &vv, &T->x);
+    f2_mul(&A, &uu, &T->z);
+    f2_sub(&A, &A, &vvv);
+    f2_sub(&A, &A, &R);
+    f2_sub(&A, &A, &R);
+    f2_mul(&T->x, &v, &A);
+    f2_sub(&t, &R, &A);
+    f2_mul(&t, &u, &t);
+    f2_mul(&vvv, &vvv, &T->y);
+    f2_sub(&T->y, &t, &vvv);
+    f2_mul(&T->z, &T->z, &vv);
+    f2_mul(&T->z, &T->z, &v);
+    mul_line(f, &l0, &l1, &l4);
+}
+static void miller(fp12 *f, const fp *xp, const fp *yp, const fp2 *xq, const fp2 *yq) {
+    g2p T = {*xq, *yq, {ONE, {{0}}}};
+    f12_one(f);
+    for (int b = 62; b >= 0; --b) {
+        f12_sqr(f, f);
+        dbl_step(&T, f, xp, yp);
+        if ((XABS >> b) & 1) add_step(&T, f, xq, yq, xp, yp);
+    }
+    f12_conj(f, f);
+}
+static void final_exp(fp12 *out, const fp12 *f) {
+    fp12 r, t, y0, y1, y2, y3;
+    f12_inv(&t, f);
+    f12_conj(&r, f);
+    f12_mul(&r, &r, &t);
+    f12_frob(&t, &r, 2);
+    f12_mul(&r, &t, &r);
+    f12_sqr(&y0, &r);
+    f12_exp_by_x(&y1, &y0, 0);
+    f12_exp_by_x(&y2, &y1, 1);
+    f12_conj(&y3, &r);
+    f12_mul(&y1, &y1, &y3);
+    f12_conj(&y1, &y1);
+    f12_mul(&y1, &y1, &y2);
+    f12_exp_by_x(&y2, &y1, 0);
+    f12_exp_by_x(&y3, &y2, 0);
+    f12_conj(&y1, &y1);
+    f12_mul(&y3, &y3, &y1);
+    f12_conj(&y1, &y1);
+    f12_frob(&y1, &y1, 3);
+    f12_frob(&y2, &y2, 2);
+    f12_mul(&y1, &y1, &y2);
+    f12_exp_by_x(&y2, &y3, 0);
+    f12_mul(&y2, &y2, &y0);
+    f12_mul(&y2, &y2, &r);
+    f12_mul(&y1, &y1, &y2);
+    f12_frob(&y2, &y3, 1);
+    f12_mul(out, &y1, &y2);
+}
+
+/* ---------------------------------------------------------------- init / encodings */
+static void bn_mul(uint64_t *r, const uint64_t *a, int na, const uint64_t *b, int nb) {
+    memset(r, 0, sizeof(uint64_t) * (na + nb));
+    for (int i = 0; i < na; ++i) {
+        u128 c = 0;
+        for (int j = 0; j < nb; ++j) {
+            c = (u128)a[i] * b[j] + r[i + j] + (c >> 64);
+            r[i + j] = (uint64_t)c;
+        }
+        r[i + nb] = (uint64_t)(c >> 64);
+    }
+}
+static void bn_div_small(uint64_t *a, int n, uint64_t d) {
+    u128 rem = 0;
+    for (int i = n - 1; i >= 0; --i) {
+        u128 cur = (rem << 64) | a[i];
+        a[i] = (uint64_t)(cur / d);
+        rem = cur % d;
+    }
+}
+static void to_mont(fp *r, const fp *a) { fp_mul(r, a, &R2); }
+static void from_mont(fp *r, const fp *a) {
+    fp one;
+    memset(&one, 0, sizeof one);
+    one.l[0] = 1;
+    fp_mul(r, a, &one);
+}
+
+void bls_c_init(void) {
+    if (inited) return;
+    uint64_t inv = 1;   /* Newton: inv = p^-1 mod 2^64 */
+    for (int i = 0; i < 7; ++i) inv *= 2 - P[0] * inv;
+    INV = (uint64_t)0 - inv;
+    /* R2 = 2^768 mod p by doubling */
+    uint64_t t[7] = {1, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 768; ++i) {
+        uint64_t c = 0;
+        for (int j = 0; j < 6; ++j) {
+            uint64_t nc = t[j] >> 63;
+            t[j] = (t[j] << 1) | c;
+            c = nc;
+        }
+        if (c || geq_p(t)) sub_p(t);
+    }
+    memcpy(R2.l, t, 48);
+    fp one1;
+    memset(&one1, 0, sizeof one1);
+    one1.l[0] = 1;
+    to_mont(&ONE, &one1);
+    fp four = one1;
+    four.l[0] = 4;
+    to_mont(&B1, &four);
+    /* Frobenius coefficients xi^((p^k-1)/3), xi^(2(p^k-1)/3), xi^((p^k-1)/6) */
+    fp2 xi = {ONE, ONE};
+    uint64_t pk[24] = {0}, tmp[24];
+    pk[0] = 1;
+    int npk = 1;
+    for (int k = 0; k < 4; ++k) {
+        uint64_t e3[24], e6[24], e23[24];
+        memcpy(e3, pk, sizeof pk);
+        /* pk - 1 (pk >= 1) */
+        for (int i = 0; i < 24; ++i) {
+            if (e3[i]--) break;
+        }
+        memcpy(e6, e3, sizeof e3);
+        memcpy(e23, e3, sizeof e3);
+        bn_div_small(e3, 24, 3);
+        bn_div_small(e6, 24, 6);
+        bn_div_small(e23, 24, 3);
+        /* e23 = 2 * e3 */
+        uint64_t c = 0;
+        for (int i = 0; i < 24; ++i) {
+            uint64_t nc = e23[i] >> 63;
+            e23[i] = (e23[i] << 1) | c;
+            c = nc;
+        }
+        f2_pow(&F6C1[k], &xi, e3, 24);
+        f2_pow(&F6C2[k], &xi, e23, 24);
+        f2_pow(&F12C1[k], &xi, e6, 24);
+        if (k == 3) break;
+        bn_mul(tmp, pk, npk, P, 6);
+        npk += 6;
+        memset(pk, 0, sizeof pk);
+        memcpy(pk, tmp, sizeof(uint64_t) * npk);
+    }
+    inited = 1;
+}
+
+static int load_be48(fp *r, const uint8_t *s, uint8_t top_mask) {
+    uint8_t b[48];
+    memcpy(b, s, 48);
+    b[0] &= top_mask;
+    fp v;
+    for (int w = 0; w < 6; ++w) {
+        uint64_t x = 0;
+        for (int q = 0; q < 8; ++q) x = (x << 8) | b[40 - 8 * w + q];
+        v.l[w] = x;
+    }
+    if (geq_p(v.l)) return 0;
+    to_mont(r, &v);
+    return 1;
+}
+static void store_be48(uint8_t *d, const fp *a) {
+    fp v;
+    from_mont(&v, a);
+    for (int w = 0; w < 6; ++w)
+        for (int q = 0; q < 8; ++q) d[40 - 8 * w + q] = (uint8_t)(v.l[w] >> (56 - 8 * q));
+}
+static int zero_rest(const uint8_t *s, int n) {
+    if (s[0] & 0x1F) return 0;
+    for (int i = 1; i < n; ++i)
+        if (s[i]) return 0;
+    return 1;
+}
+/* 0 ok, 1 infinity, 2 invalid */
+static int dec_g1(const uint8_t *s, fp *x, fp *y) {
+    if (s[0] & 0xA0) return 2;
+    if (s[0] & 0x40) return zero_rest(s, 96) ? 1 : 2;
+    if (!load_be48(x, s, 0x1F) || !load_be48(y, s + 48, 0xFF)) return 2;
+    fp l, r;
+    fp_mul(&l, y, y);
+    fp_mul(&r, x, x);
+    fp_mul(&r, &r, x);
+    fp_add(&r, &r, &B1);
+    return fp_eq(&l, &r) ? 0 : 2;
+}
+static int dec_g2(const uint8_t *s, fp2 *x, fp2 *y) {
+    if (s[0] & 0xA0) return 2;
+    if (s[0] & 0x40) return zero_rest(s, 192) ? 1 : 2;
+    if (!load_be48(&x->c1, s, 0x1F) || !load_be48(&x->c0, s + 48, 0xFF) ||
+        !load_be48(&y->c1, s + 96, 0xFF) || !load_be48(&y->c0, s + 144, 0xFF))
+        return 2;
+    fp2 l, r, b = {B1, B1};
+    f2_sqr(&l, y);
+    f2_sqr(&r, x);
+    f2_mul(&r, &r, x);
+    f2_add(&r, &r, &b);
+    return (fp_eq(&l.c0, &r.c0) && fp_eq(&l.c1, &r.c1)) ? 0 : 2;
+}
+
+/* e(g1, g2) -> 576 GT bytes (tower order, big-endian); returns 0 ok, 2 invalid */
+int bls_c_pairing(const uint8_t *g1, const uint8_t *g2, uint8_t *gt) {
+    bls_c_init();
+    fp xp, yp;
+    fp2 xq, yq;
+    int s1 = dec_g1(g1, &xp, &yp), s2 = dec_g2(g2, &xq, &yq);
+    fp12 f, e;
+    f12_one(&f);
+    if (s1 == 0 && s2 == 0) miller(&f, &xp, &yp, &xq, &yq);
+    final_exp(&e, &f);
+    const fp2 *c[6] = {&e.c0.c0, &e.c0.c1, &e.c0.c2, &e.c1.c0, &e.c1.c1, &e.c1.c2};
+    for (int k = 0; k < 6; ++k) {
+        store_be48(gt + 96 * k, &c[k]->c0);
+        store_be48(gt + 96 * k + 48, &c[k]->c1);
+    }
+    return (s1 == 2 || s2 == 2) ? 2 : 0;
+}
+
+/* e(a, b) == e(c, d): 1 equal, 0 not, 2 invalid point */
+int bls_c_check(const uint8_t *a, const uint8_t *b, const uint8_t *c, const uint8_t *d) {
+    bls_c_init();
+    fp xa, ya, xc, yc;
+    fp2 xb, yb, xd, yd;
+    int sa = dec_g1(a, &xa, &ya), sb = dec_g2(b, &xb, &yb);
+    int sc = dec_g1(c, &xc, &yc), sd = dec_g2(d, &xd, &yd);
+    if (sa == 2 || sb == 2 || sc == 2 || sd == 2) return 2;
+    fp12 f1, f2, e;
+    f12_one(&f1);
+    f12_one(&f2);
+    if (sa == 0 && sb == 0) miller(&f1, &xa, &ya, &xb, &yb);
+    if (sc == 0 && sd == 0) {
+        fp_neg(&yc, &yc);
+        miller(&f2, &xc, &yc, &xd, &yd);
+    }
+    f12_mul(&f1, &f1, &f2);
+    final_exp(&e, &f1);
+    return f12_is_one(&e);
+}
+
+typedef struct {
+    const uint8_t *g1, *g2;
+    size_t lo, hi;
+    uint8_t *ok;
+} job;
+static void *run_jobs(void *p) {
+    job *j = (job *)p;
+    for (size_t i = j->lo; i < j->hi; ++i)
+        j->ok[i] = (uint8_t)bls_c_check(j->g1 + 192 * i, j->g2 + 384 * i, j->g1 + 192 * i + 96,
+                                        j->g2 + 384 * i + 192);
+    return 0;
+}
+/* count checks in hbrbc_pairing_check_batch's layout (g1: a_i, c_i; g2: b_i,
+ * d_i) on `threads` threads; ok[i] as bls_c_check. */
+void bls_c_check_batch(const uint8_t *g1, const uint8_t *g2, size_t count, uint8_t *ok,
+                       int threads) {
+    bls_c_init();
+    if (threads < 1) threads = 1;
+    pthread_t th[256];
+    job jb[256];
+    if (threads > 256) threads = 256;
+    for (int t = 0; t < threads; ++t) {
+        jb[t] = (job){g1, g2, count * t / threads, count * (t + 1) / threads, ok};
+        pthread_create(&th[t], 0, run_jobs, &jb[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+}

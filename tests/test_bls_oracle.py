@@ -67,3 +67,22 @@ def test_oracle_reproduces_golden(idx):
 def test_golden_g1_encoding_of_generator_matches_product_constant():
     from hbbft_amd import threshold
     assert threshold.G1_ONE == B.g1_bytes(B.G1_GEN)
+
+
+def test_c_restatement_matches_golden_and_python():
+    """oracle/bls_pairing.c (the bench's f4 CPU baseline) against the golden GT
+    bytes of the Python restatement, the check outcomes, and the same
+    encoding rejections as the product."""
+    from oracle import bls_c
+    for v in GOLD["pairings"]:
+        gt, st = bls_c.pairing(bytes.fromhex(v["g1"]), bytes.fromhex(v["g2"]))
+        assert st == 0 and gt.hex() == v["gt"]
+    for c in GOLD["checks"] + GOLD["bench_pool"][:8]:
+        assert bls_c.check(*(bytes.fromhex(c[k]) for k in "abcd")) == (1 if c["expect"] else 0)
+    g1, g2 = B.g1_bytes(B.G1_GEN), B.g2_bytes(B.G2_GEN)
+    bad = bytearray(g1)
+    bad[-1] ^= 1
+    assert bls_c.check(bytes(bad), g2, g1, g2) == 2
+    assert bls_c.check(bytes([g1[0] | 0x80]) + g1[1:], g2, g1, g2) == 2
+    gt, st = bls_c.pairing(B.g1_bytes(None), g2)
+    assert st == 0 and gt == B.gt_bytes(B.F12_ONE)
