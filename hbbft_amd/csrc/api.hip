@@ -443,6 +443,14 @@ int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, const RowM
         }
     }
     StageTimer t(c, HBRBC_STAGE_TREE_LEVELS, s);
+    // HBRBC_TREE_LEVELS_LDS=1: every level in one LDS-reduced launch (measured
+    // slower at cfg3: 0.80 vs 0.31 ms per step -- the upper levels idle most
+    // lanes of a block, while per-level launches keep every lane busy)
+    const char *lv = getenv("HBRBC_TREE_LEVELS_LDS");
+    if (n <= 512 && lv && !std::strcmp(lv, "1")) {
+        HB_HIP(launch_tree_levels(nodes, node_inst_stride, n, count, s));
+        return HBRBC_OK;
+    }
     size_t off = 0, sz = n;
     while (sz > 1) {
         const size_t nsz = (sz + 1) / 2;

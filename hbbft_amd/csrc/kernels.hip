@@ -508,6 +508,56 @@ __global__ __launch_bounds__(kBlock) void tree_level_kernel(
     store_digest(ns + (size_t)(cur_off + j) * 32, d);
 }
 
+// Every level of whole trees in one launch, reduced in LDS (north_star item 4),
+// after the leaf-hash kernel has written level 0: lane = (instance li of the
+// block, pair t); a block holds ipb = 256 / ceil(n/2) instances.  Level 0 comes
+// in from the node slab, each level is one pair hash per lane between two LDS
+// buffers and goes out to the slab (odd last node promoted, merkle.rs:128-134).
+__global__ __launch_bounds__(kBlock) void tree_levels_kernel(
+    uint8_t *__restrict__ nodes, size_t node_inst_stride, uint32_t n, uint32_t half,
+    uint32_t ipb, size_t count) {
+    __shared__ uint4 lvl[2][2 * kBlock][2];   // two levels of up to 512 digests: 32 KB
+    const uint32_t li = threadIdx.x / half, t = threadIdx.x - li * half;
+    const size_t inst = (size_t)blockIdx.x * ipb + li;
+    const bool active = li < ipb && inst < count;   // every lane meets every barrier
+    uint8_t *ns = nodes + inst * node_inst_stride;
+    const uint32_t base = li * 2 * half;
+    if (active) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t j = 2 * t + e;
+            if (j < n) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(ns + (size_t)j * 32);
+                lvl[0][base + j][0] = src[0];
+                lvl[0][base + j][1] = src[1];
+            }
+        }
+    }
+    uint32_t off = 0, sz = n, cur = 0;
+    while (sz > 1) {                // the same trip count in every lane
+        __syncthreads();
+        const uint32_t nsz = (sz + 1) >> 1;
+        if (active && t < nsz) {
+            const uint4 a0 = lvl[cur][base + 2 * t][0], a1 = lvl[cur][base + 2 * t][1];
+            uint32_t a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w}, o[8];
+            if (2 * t + 1 < sz) {
+                const uint4 b0 = lvl[cur][base + 2 * t + 1][0], b1 = lvl[cur][base + 2 * t + 1][1];
+                const uint32_t b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+                sha3_256_pair(a, b, o);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 8; ++w) o[w] = a[w];
+            }
+            store_digest(ns + (size_t)(off + sz + t) * 32, o);
+            lvl[cur ^ 1][base + t][0] = make_uint4(o[0], o[1], o[2], o[3]);
+            lvl[cur ^ 1][base + t][1] = make_uint4(o[4], o[5], o[6], o[7]);
+        }
+        off += sz;
+        sz = nsz;
+        cur ^= 1u;
+    }
+}
+
 // ---------------------------------------------------------------- proofs --
 __global__ __launch_bounds__(kBlock) void proofs_kernel(
     const uint8_t *__restrict__ nodes, size_t node_inst_stride, uint32_t n, size_t count,
@@ -1120,6 +1170,19 @@ hipError_t launch_tree_level(uint8_t *nodes, size_t node_inst_stride, size_t pre
     hipLaunchKernelGGL(tree_level_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock), 0,
                        s, nodes, node_inst_stride, (uint32_t)prev_off, (uint32_t)prev_size,
                        (uint32_t)cur_off, (uint32_t)cur_size, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_tree_levels(uint8_t *nodes, size_t node_inst_stride, size_t n, size_t count,
+                              hipStream_t s) {
+    if (count == 0 || n < 2) return hipSuccess;
+    if (n > 2 * kBlock) return hipErrorInvalidValue;
+    const uint32_t half = (uint32_t)((n + 1) / 2);
+    const uint32_t ipb = kBlock / half;
+    const size_t blocks = (count + ipb - 1) / ipb;
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tree_levels_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, nodes,
+                       node_inst_stride, (uint32_t)n, half, ipb, count);
     return hipGetLastError();
 }
 

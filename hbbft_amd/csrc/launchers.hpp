@@ -111,6 +111,9 @@ hipError_t launch_ragged_hash(const uint8_t *base, const uint64_t *offsets,
 hipError_t launch_tree_level(uint8_t *nodes, size_t node_inst_stride, size_t prev_off,
                              size_t prev_size, size_t cur_off, size_t cur_size, size_t count,
                              hipStream_t s);
+// Every level above level 0 in one launch, reduced in LDS (n <= 512).
+hipError_t launch_tree_levels(uint8_t *nodes, size_t node_inst_stride, size_t n, size_t count,
+                              hipStream_t s);
 hipError_t launch_proofs(const uint8_t *nodes, size_t node_inst_stride, size_t n, size_t count,
                          uint8_t *digests, size_t dslots, uint8_t *ndig, hipStream_t s);
 // Proof (i, jj): value row r = rows ? rows[jj] : jj of instance i at

@@ -121,18 +121,22 @@ def test_merkle_ragged_values_vs_oracle(torch_cuda):
         assert [d for level in lv for d in level] == [r.tobytes() for r in ref]
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
-def test_merkle_batch_level_forms_vs_oracle(torch_cuda, monkeypatch, fused):
-    """hbrbc_merkle_batch with one launch per level (default) and with the
-    leaves and levels in one launch, levels reduced in LDS
-    (HBRBC_MERKLE_FUSED=1; whole instances per 256-lane block, odd nodes
-    promoted): every node of every tree equals the oracle's, for validator
-    counts that fill a block exactly, nearly, or not at all (fallback)."""
+@pytest.mark.parametrize("fused,levels", [("0", "1"), ("0", "0"), ("1", "1")])
+def test_merkle_batch_level_forms_vs_oracle(torch_cuda, monkeypatch, fused, levels):
+    """hbrbc_merkle_batch in its three forms: leaf kernel + one launch per
+    level (default), leaf kernel + all levels in one LDS-reduced launch
+    (HBRBC_TREE_LEVELS_LDS=1), and leaves and levels in one launch
+    (HBRBC_MERKLE_FUSED=1); whole instances per 256-lane block, odd nodes
+    promoted: every node of every tree equals the oracle's, for validator
+    counts that fill a block exactly, nearly, or not at all, and instance
+    counts that leave a partial last block."""
     torch = torch_cuda
     monkeypatch.setenv("HBRBC_MERKLE_FUSED", fused)
+    monkeypatch.setenv("HBRBC_TREE_LEVELS_LDS", levels)
     rng = np.random.default_rng(17)
-    for n, L, count in [(2, 5, 3), (4, 300, 5), (7, 136, 9), (16, 1000, 17), (64, 2000, 5),
-                        (100, 77, 3), (128, 513, 3), (250, 40, 2), (256, 272, 2)]:
+    for n, L, count in [(2, 5, 3), (3, 9, 7), (4, 300, 5), (5, 17, 11), (7, 136, 9),
+                        (9, 40, 29), (16, 1000, 17), (17, 33, 8), (33, 12, 9), (64, 2000, 5),
+                        (64, 100, 13), (100, 77, 3), (128, 513, 3), (250, 40, 2), (256, 272, 3)]:
         rb = hb.RbcBatch(n, device=0)
         stride = (L + 15) // 16 * 16
         data = rng.integers(0, 256, (count, n, stride), dtype=np.uint8)
