@@ -552,7 +552,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
 
 # --------------------------------------------------------------------- main --
 # ------------------------------------------------ f4: threshold-decrypt checks --
-F4_CHECKS = 131072     # 32 epochs x 64 ciphertexts x 64 decryption shares (N=64)
+F4_CHECKS = 262144     # 64 epochs x 64 ciphertexts x 64 decryption shares (N=64)
 F4_METRIC = "threshold-decrypt share verifications/s (BLS12-381 pairing checks)"
 
 
