@@ -677,8 +677,8 @@ def run_threshold(args, rank, world, dev):
             "device_ms_per_step": ev_ms / args.f4_steps, "pairings_per_step": 2 * n,
             "scaling": "weak", "dtype": "u32 (12-limb Montgomery Fp)",
             "config": {"workload": "f4: verify_decryption_share e(share, H) == e(pk_i, W), "
-                                   "%d checks per GPU per step (32 epochs x 64 ciphertexts x 64 "
-                                   "shares, N=64)" % n, "checks_per_gpu": n},
+                                   "%d checks per GPU per step (%d epochs x 64 ciphertexts x 64 "
+                                   "shares, N=64)" % (n, n // 4096), "checks_per_gpu": n},
             "data": "the 32 fixture checks of tests/golden/bls_vectors.json tiled "
                     "(one in four tampered); outcomes verified exactly",
             "roofline": roof}
