@@ -1914,6 +1914,13 @@ static int pairing_run(const uint8_t *g1, const uint8_t *g2, size_t n_pair, size
         return fail(HBRBC_E_NO_DEVICE, "no HIP device visible");
     uint32_t *ws = static_cast<uint32_t *>(workspace);
     uint8_t *st = static_cast<uint8_t *>(workspace) + round_up(n_pair * 576, 256);
+    const char *mm = getenv("HBRBC_PAIR_MULTI");   // 0: one lane per pairing (A/B)
+    if (per_out == 2 && !(mm && !std::strcmp(mm, "0"))) {
+        // checks: one lane per check, both Miller loops sharing f's squarings
+        HB_HIP(launch_pairing_miller2(g1, g2, n_out, ws, st, s));
+        HB_HIP(launch_pairing_final(ws, n_out, n_out, 1, st, gt_out, ok_out, s));
+        return HBRBC_OK;
+    }
     HB_HIP(launch_pairing_miller(g1, 96, g2, 192, n_pair, per_out == 2, ws, st, s));
     if (status_out) HB_HIP(hipMemcpyAsync(status_out, st, n_pair, hipMemcpyDeviceToDevice, s));
     HB_HIP(launch_pairing_final(ws, n_pair, n_out, per_out, st, gt_out, ok_out, s));

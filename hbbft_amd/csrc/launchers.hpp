@@ -224,6 +224,8 @@ hipError_t launch_wire_decode(const WireDecodeArgs &a, hipStream_t s);
 hipError_t launch_pairing_miller(const uint8_t *g1, size_t g1_stride, const uint8_t *g2,
                                  size_t g2_stride, size_t n, int pair_inputs, uint32_t *ws,
                                  uint8_t *status, hipStream_t s);
+hipError_t launch_pairing_miller2(const uint8_t *g1, const uint8_t *g2, size_t count,
+                                  uint32_t *ws, uint8_t *status, hipStream_t s);
 hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_out, int per_out,
                                 const uint8_t *status, uint8_t *gt_out, uint8_t *ok_out,
                                 hipStream_t s);

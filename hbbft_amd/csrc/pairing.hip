@@ -720,6 +720,51 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4
     store_f12(ws, n, i, f);
 }
 
+// Kernel 1b: one lane per check e(a, b) == e(c, d) (g1 holds a, c and g2 b, d
+// at rows 2i, 2i+1): the two Miller loops of f_a,b * f_-c,d share one
+// squaring of f per step (a multi-Miller loop; the product is what the final
+// exponentiation needs).  An infinity drops its pairing's lines (factor 1).
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void miller2_kernel(
+    const uint8_t *__restrict__ g1, const uint8_t *__restrict__ g2, size_t count,
+    uint32_t *__restrict__ ws, uint8_t *__restrict__ status) {
+    const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    if (i >= count) return;
+    Fp xa, ya, xc, yc;
+    Fp2 xb, yb, xd, yd;
+    const int sa = decode_g1(g1 + (2 * i) * 96, xa, ya);
+    const int sc = decode_g1(g1 + (2 * i + 1) * 96, xc, yc);
+    const int sb = decode_g2(g2 + (2 * i) * 192, xb, yb);
+    const int sd = decode_g2(g2 + (2 * i + 1) * 192, xd, yd);
+    const bool bad = sa == PT_BAD || sb == PT_BAD || sc == PT_BAD || sd == PT_BAD;
+    const bool on1 = !bad && sa == PT_OK && sb == PT_OK;
+    const bool on2 = !bad && sc == PT_OK && sd == PT_OK;
+    Fp12 f;
+    fp12_one(f);
+    if (on1 || on2) {
+        fp_neg(yc, yc);   // e(-c, d) = e(c, d)^-1
+        G2Proj T1, T2;
+        T1.x = xb;
+        T1.y = yb;
+        fp_set(T1.z.c0, kOne);
+        fp_zero(T1.z.c1);
+        T2.x = xd;
+        T2.y = yd;
+        T2.z = T1.z;
+        for (int b = 62; b >= 0; --b) {
+            fp12_sqr(f, f);
+            if (on1) miller_dbl(T1, f, xa, ya);
+            if (on2) miller_dbl(T2, f, xc, yc);
+            if ((kXAbs >> b) & 1u) {
+                if (on1) miller_add(T1, f, xb, yb, xa, ya);
+                if (on2) miller_add(T2, f, xd, yd, xc, yc);
+            }
+        }
+        fp12_conj(f, f);
+    }
+    status[i] = bad ? PT_BAD : PT_OK;
+    store_f12(ws, count, i, f);
+}
+
 // The crate's final exponentiation (Bls12::final_exponentiation): easy part
 // f^((p^6 - 1)(p^2 + 1)), then the hard-part chain.
 DEV void final_exp(Fp12 &out, const Fp12 &f) {
@@ -810,6 +855,15 @@ hipError_t launch_pairing_miller(const uint8_t *g1, size_t g1_stride, const uint
     const unsigned blocks = (unsigned)((n + kPairBlock - 1) / kPairBlock);
     hipLaunchKernelGGL(miller_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, g1_stride, g2, g2_stride, n,
                        pair_inputs, ws, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairing_miller2(const uint8_t *g1, const uint8_t *g2, size_t count,
+                                  uint32_t *ws, uint8_t *status, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(miller2_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, g2, count, ws,
+                       status);
     return hipGetLastError();
 }
 

@@ -109,3 +109,28 @@ def test_per_call_rejects_invalid_point():
     with pytest.raises(RseError):
         T.pairing_check(bytes(bad), B.g2_bytes(B.G2_GEN), B.g1_bytes(B.G1_GEN),
                         B.g2_bytes(B.G2_GEN))
+
+
+@pytest.mark.parametrize("multi", ["1", "0"])
+def test_check_batch_infinity_and_invalid(monkeypatch, multi):
+    """Checks whose points include infinity (that pairing is 1) or an invalid
+    encoding (outcome 2), on the one-lane-per-check multi-Miller kernel
+    (default) and on one lane per pairing (HBRBC_PAIR_MULTI=0)."""
+    from hbbft_amd import threshold as T
+    monkeypatch.setenv("HBRBC_PAIR_MULTI", multi)
+    P, Q = B.g1_mul(B.G1_GEN, 3), B.g2_mul(B.G2_GEN, 5)
+    P15 = B.g1_mul(B.G1_GEN, 15)
+    inf1, inf2 = B.g1_bytes(None), B.g2_bytes(None)
+    bad = bytearray(B.g1_bytes(P))
+    bad[-1] ^= 1
+    cases = [
+        ((B.g1_bytes(P), B.g2_bytes(Q), B.g1_bytes(P15), B.g2_bytes(B.G2_GEN)), 1),
+        ((inf1, B.g2_bytes(Q), B.g1_bytes(P), inf2), 1),          # 1 == 1
+        ((B.g1_bytes(P), B.g2_bytes(Q), inf1, B.g2_bytes(Q)), 0),  # e(P,Q) != 1
+        ((inf1, inf2, inf1, inf2), 1),
+        ((bytes(bad), B.g2_bytes(Q), B.g1_bytes(P), B.g2_bytes(Q)), 2),
+        ((B.g1_bytes(P), B.g2_bytes(Q), B.g1_bytes(P), B.g2_bytes(Q)), 1),
+    ]
+    g1 = _t([x for (a, b, c, d), _ in cases for x in (a, c)], 96)
+    g2 = _t([x for (a, b, c, d), _ in cases for x in (b, d)], 192)
+    assert T.pairing_check_batch(g1, g2).cpu().tolist() == [e for _, e in cases]
