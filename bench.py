@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--f4-checks", type=int, default=F4_CHECKS,
                     help="f4 leg: pairing checks per GPU per step (0 = skip the leg)")
     ap.add_argument("--f4-steps", type=int, default=3)
+    ap.add_argument("--no-cfg4", action="store_true",
+                    help="skip the cfg4 validator-sharded object of the default cfg3 line")
     ap.add_argument("--streams", type=int, default=1,
                     help="instance mode: sub-batches per step, each on its own HIP stream")
     ap.add_argument("--vsubs", type=int, default=4,
@@ -670,8 +672,9 @@ def run_threshold(args, rank, world, dev):
         roof = {"bound": "valu", "achieved": rate / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                 "unit": "T lane-ops/s", "frac": rate / VALU_PEAK_OPS, "traffic": None,
                 "ops_per_check": ops, "ops_per_check_source": src,
-                "note": "miller_kernel + final_exp_kernel together, timed with HIP events on "
-                        "the launch stream; the mix is ~20% v_mad_u64_u32 (multi-pass)"}
+                "note": "miller2_kernel + final_exp_kernel together, timed with HIP events on "
+                        "the launch stream; ~55% of the mix issues at half rate "
+                        "(v_mad_u64_u32, v_addc_co_u32; profiles/r2c_valu_microbench.txt)"}
     return {"metric": F4_METRIC, "value": checks / wall, "unit": "checks/s",
             "ms_per_step": wall / args.f4_steps * 1e3, "steps": args.f4_steps,
             "device_ms_per_step": ev_ms / args.f4_steps, "pairings_per_step": 2 * n,
@@ -730,6 +733,18 @@ def main():
                 vobj = {"error": "%s: %s" % (type(e).__name__, e)}
                 print("bench: validator-sharded run failed: %r" % (e,), file=sys.stderr)
 
+    # cfg4 (N=128, validators sharded over the ranks, RCCL all-to-all + all-gather)
+    # rides along the default cfg3 line so the driver's multi-GPU runs measure it
+    v4 = None
+    if args.mode == "both" and args.config == "cfg3" and not args.no_cfg4:
+        torch.cuda.empty_cache()
+        n4, plen4, _, _, vcount4 = CONFIGS["cfg4"]
+        try:
+            v4 = run_validators(args, n4, plen4, args.vcount or vcount4, rank, world, dev, local)
+        except Exception as e:  # noqa: BLE001  (secondary object: keep the headline line)
+            v4 = {"error": "%s: %s" % (type(e).__name__, e)}
+            print("bench: cfg4 validator-sharded run failed: %r" % (e,), file=sys.stderr)
+
     f4 = None
     if args.f4_checks > 0:
         torch.cuda.empty_cache()
@@ -766,6 +781,8 @@ def main():
                     vobj["cpu_baseline"] = dict(cpu, note="the same per-instance pipeline; the "
                                                 "CPU leg decodes each instance once")
                 line["validators"] = vobj
+            if v4 is not None:
+                line["validators_cfg4"] = v4
             if f4 is not None:
                 line["threshold_decrypt"] = f4
         else:
