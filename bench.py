@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0          # MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy
 VALU_PEAK_OPS = 78.6e12        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (32-bit lane-ops/s)
 KECCAK_OPS_PER_PERM = 4320     # static count: 180 VALU per round x 24 rounds
 # measured ceiling of the Keccak-f[1600] round code itself (register-only loop,
@@ -226,7 +227,8 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
          "hbm": {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": hbm_gbs / HBM_PEAK_GBS, "alg_bytes_per_launch": alg[dom]},
          "pipeline_alg_bytes_per_step": step_bytes, "stages": per_stage,
-         "pipeline_hbm_frac": step_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS}
+         "pipeline_hbm_frac": step_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS,
+         "pipeline_frac_of_measured_copy": step_bytes / (elapsed / steps) / 1e9 / HBM_COPY_GBS}
     if dom in perms:
         opp, src = valu_ops_per_perm()
         pps = perms[dom] / t
