@@ -23,6 +23,9 @@ def lib():
         L.bls_c_check_batch.restype = None
         L.bls_c_check_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
                                         ctypes.c_void_p, ctypes.c_int]
+        L.bls_c_pairing_batch.restype = None
+        L.bls_c_pairing_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -45,3 +48,12 @@ def check_batch(g1, g2, count, threads):
     ok = ctypes.create_string_buffer(count)
     lib().bls_c_check_batch(bytes(g1), bytes(g2), count, ok, threads)
     return ok.raw
+
+
+def pairing_batch(g1, g2, count, threads):
+    """count pairings (uncompressed encodings, concatenated) -> (gt bytes
+    [count * 576], status bytes [count])."""
+    gt = ctypes.create_string_buffer(576 * count)
+    st = ctypes.create_string_buffer(count)
+    lib().bls_c_pairing_batch(bytes(g1), bytes(g2), count, gt, st, threads)
+    return gt.raw, st.raw

@@ -661,3 +661,29 @@ void bls_c_check_batch(const uint8_t *g1, const uint8_t *g2, size_t count, uint8
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
 }
+
+typedef struct {
+    const uint8_t *g1, *g2;
+    size_t lo, hi;
+    uint8_t *gt, *st;
+} pjob;
+static void *run_pjobs(void *p) {
+    pjob *j = (pjob *)p;
+    for (size_t i = j->lo; i < j->hi; ++i)
+        j->st[i] = (uint8_t)bls_c_pairing(j->g1 + 96 * i, j->g2 + 192 * i, j->gt + 576 * i);
+    return 0;
+}
+/* count pairings e(g1[i], g2[i]) -> gt + 576 i, status st[i], on `threads` threads */
+void bls_c_pairing_batch(const uint8_t *g1, const uint8_t *g2, size_t count, uint8_t *gt,
+                         uint8_t *st, int threads) {
+    bls_c_init();
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    pjob jb[256];
+    for (int t = 0; t < threads; ++t) {
+        jb[t] = (pjob){g1, g2, count * t / threads, count * (t + 1) / threads, gt, st};
+        pthread_create(&th[t], 0, run_pjobs, &jb[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], 0);
+}

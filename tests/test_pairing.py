@@ -134,3 +134,22 @@ def test_check_batch_infinity_and_invalid(monkeypatch, multi):
     g1 = _t([x for (a, b, c, d), _ in cases for x in (a, c)], 96)
     g2 = _t([x for (a, b, c, d), _ in cases for x in (b, d)], 192)
     assert T.pairing_check_batch(g1, g2).cpu().tolist() == [e for _, e in cases]
+
+
+def test_pairing_batch_at_size_vs_c_restatement():
+    """4096 GT values (a 64 x 64 grid of pool points) bit-exact against the C
+    restatement (oracle/bls_pairing.c, itself pinned to the Python oracle's
+    golden bytes in tests/test_bls_oracle.py)."""
+    import os
+    from hbbft_amd import threshold as T
+    from oracle import bls_c
+    rng = random.Random(11)
+    P = [B.g1_bytes(B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))) for _ in range(64)]
+    Q = [B.g2_bytes(B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))) for _ in range(64)]
+    g1b = b"".join(P[i % 64] for i in range(4096))
+    g2b = b"".join(Q[i // 64] for i in range(4096))
+    gt, st = T.pairing_batch(_t([g1b[96 * i:96 * i + 96] for i in range(4096)], 96),
+                             _t([g2b[192 * i:192 * i + 192] for i in range(4096)], 192))
+    ref_gt, ref_st = bls_c.pairing_batch(g1b, g2b, 4096, min(16, os.cpu_count() or 1))
+    assert st.cpu().numpy().tobytes() == ref_st == b"\0" * 4096
+    assert gt.cpu().numpy().tobytes() == ref_gt
