@@ -626,29 +626,47 @@ def f4_cpu_baseline(pool, reps, target_s=2.0):
 
 
 def run_threshold(args, rank, world, dev):
-    """f4 leg: F4_CHECKS verify_decryption_share checks per GPU per step, e(share,
-    H) == e(pk_i, W), through hbrbc_pairing_check_batch; inputs tile the 32
-    committed fixture checks (tests/golden/bls_vectors.json, one in four
-    tampered), outcomes checked exactly after warm-up."""
+    """f4 leg: F4_CHECKS verify_decryption_share checks per GPU per step in
+    hbbft's shape -- groups of 64 shares checked against one ciphertext's H and
+    W (threshold_decrypt.rs:204-229) -- e(share, H) == e(pk_i, W): every step
+    prepares each ciphertext's H and W (hbrbc_g2_prepare) and checks the
+    shares against them (hbrbc_pairing_check_prepared).  Inputs tile the 4
+    committed fixture groups (tests/golden/bls_vectors.json, one share in
+    eight tampered); outcomes are checked exactly after warm-up.  The plain
+    per-check form (hbrbc_pairing_check_batch) is timed beside it."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from hbbft_amd import threshold as T
-    pool = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))["bench_pool"]
-    n = args.f4_checks
+    groups = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))["bench_groups"]
+    n = args.f4_checks // 64 * 64
+    ng = n // 64
+    g2 = np.empty((2 * ng, 192), np.uint8)
     g1 = np.empty((2 * n, 96), np.uint8)
-    g2 = np.empty((2 * n, 192), np.uint8)
-    enc = [[np.frombuffer(bytes.fromhex(c[k]), np.uint8) for k in "abcd"] for c in pool]
-    idx = (np.arange(n) + rank) % len(pool)
-    for j, e in enumerate(enc):
-        sel = np.nonzero(idx == j)[0]
-        g1[2 * sel], g2[2 * sel], g1[2 * sel + 1], g2[2 * sel + 1] = e[0], e[1], e[2], e[3]
-    expect = torch.tensor([1 if pool[j]["expect"] else 0 for j in idx], dtype=torch.uint8)
+    enc = [(np.frombuffer(bytes.fromhex(g["hash"]), np.uint8),
+            np.frombuffer(bytes.fromhex(g["w"]), np.uint8),
+            np.stack([np.frombuffer(bytes.fromhex(s["share"]), np.uint8) for s in g["shares"]]),
+            np.stack([np.frombuffer(bytes.fromhex(s["pk"]), np.uint8) for s in g["shares"]]),
+            [1 if s["expect"] else 0 for s in g["shares"]]) for g in groups]
+    expect = []
+    for q in range(ng):
+        h, w, sh, pk, ex = enc[(q + rank) % len(enc)]
+        g2[2 * q], g2[2 * q + 1] = h, w
+        g1[2 * q * 64:2 * (q + 1) * 64:2] = sh
+        g1[2 * q * 64 + 1:2 * (q + 1) * 64:2] = pk
+        expect += ex
+    expect = torch.tensor(expect, dtype=torch.uint8)
     d1, d2 = torch.from_numpy(g1).to(dev), torch.from_numpy(g2).to(dev)
-    ws = T.workspace(2 * n, dev.index)
+    ib = torch.arange(n, dtype=torch.int32, device=dev) // 64 * 2
+    idd = ib + 1
+    ws = T.workspace(n, dev.index)
     stream = torch.cuda.current_stream(dev)
+
+    def step():
+        prep = T.g2_prepare(d2)
+        return T.pairing_check_prepared(d1, prep, 2 * ng, ib, idd, ws)
     for _ in range(max(1, args.warmup)):
-        ok = T.pairing_check_batch(d1, d2, ws)
+        ok = step()
     torch.cuda.synchronize(dev)
     if not torch.equal(ok.cpu(), expect):
         raise SystemExit("bench f4: check outcomes differ from the fixtures")
@@ -659,13 +677,30 @@ def run_threshold(args, rank, world, dev):
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(args.f4_steps):
-        T.pairing_check_batch(d1, d2, ws)
+        step()
     e1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = max_over_ranks(time.perf_counter() - t0, world, dev)
     ev_ms = e0.elapsed_time(e1)
+    # the plain form on the same checks: each check carries its own G2 points
+    g2p = np.empty((2 * n, 192), np.uint8)
+    g2p[0::2] = np.repeat(g2[0::2], 64, axis=0)
+    g2p[1::2] = np.repeat(g2[1::2], 64, axis=0)
+    d2p = torch.from_numpy(g2p).to(dev)
+    wsp = T.workspace(2 * n, dev.index)
+    okp = T.pairing_check_batch(d1, d2p, wsp)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(okp.cpu(), expect)
+    p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    p0.record(stream)
+    for _ in range(args.f4_steps):
+        T.pairing_check_batch(d1, d2p, wsp)
+    p1.record(stream)
+    torch.cuda.synchronize(dev)
+    plain_ms = p0.elapsed_time(p1) / args.f4_steps
+    del d2p, wsp
     checks = world * n * args.f4_steps
     ops, src = pairing_ops_per_check()
     roof = None
@@ -674,20 +709,22 @@ def run_threshold(args, rank, world, dev):
         roof = {"bound": "valu", "achieved": rate / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                 "unit": "T lane-ops/s", "frac": rate / VALU_PEAK_OPS, "traffic": None,
                 "ops_per_check": ops, "ops_per_check_source": src,
-                "note": "miller2_kernel + final_exp_kernel together, timed with HIP events on "
-                        "the launch stream; ~55% of the mix issues at half rate "
-                        "(v_mad_u64_u32, v_addc_co_u32; profiles/r2c_valu_microbench.txt)"}
+                "note": "g2_prepare_kernel + miller_prepared_kernel + final_exp_kernel, timed "
+                        "with HIP events on the launch stream; ~55% of the mix issues at half "
+                        "rate (v_mad_u64_u32, v_addc_co_u32; profiles/r2c_valu_microbench.txt)"}
     return {"metric": F4_METRIC, "value": checks / wall, "unit": "checks/s",
             "ms_per_step": wall / args.f4_steps * 1e3, "steps": args.f4_steps,
-            "device_ms_per_step": ev_ms / args.f4_steps, "pairings_per_step": 2 * n,
+            "device_ms_per_step": ev_ms / args.f4_steps, "g2_points_prepared_per_step": 2 * ng,
+            "plain_checks": {"checks_per_s": n / (plain_ms / 1e3), "ms_per_step": plain_ms,
+                             "note": "hbrbc_pairing_check_batch, G2 points per check"},
             "scaling": "weak", "dtype": "u32 (12-limb Montgomery Fp)",
             "config": {"workload": "f4: verify_decryption_share e(share, H) == e(pk_i, W), "
-                                   "%d checks per GPU per step (%d epochs x 64 ciphertexts x 64 "
-                                   "shares, N=64)" % (n, n // 4096), "checks_per_gpu": n},
-            "data": "the 32 fixture checks of tests/golden/bls_vectors.json tiled "
-                    "(one in four tampered); outcomes verified exactly",
+                                   "%d checks per GPU per step (%d ciphertexts x 64 shares, N=64; "
+                                   "each ciphertext's H and W prepared once per step)" % (n, ng),
+                       "checks_per_gpu": n},
+            "data": "the 4 fixture groups of tests/golden/bls_vectors.json tiled "
+                    "(one share in eight tampered); outcomes verified exactly",
             "roofline": roof}
-
 
 def main():
     args = parse()
@@ -758,8 +795,9 @@ def main():
             f4 = {"error": "%s: %s" % (type(e).__name__, e)}
             print("bench: f4 leg failed: %r" % (e,), file=sys.stderr)
         if rank == 0 and world == 1 and not args.no_cpu and "error" not in f4:
-            pool = json.load(open(os.path.join(ROOT, "tests", "golden",
-                                               "bls_vectors.json")))["bench_pool"]
+            gold = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))
+            pool = [{"a": s["share"], "b": g["hash"], "c": s["pk"], "d": g["w"],
+                     "expect": s["expect"]} for g in gold["bench_groups"] for s in g["shares"][:8]]
             f4["cpu_baseline"] = f4_cpu_baseline(pool, 3)
 
     cpu = None

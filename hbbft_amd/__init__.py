@@ -130,6 +130,9 @@ def lib():
         "hbrbc_jit_decode_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p, _S]),
         "hbrbc_unframe_fused": (ctypes.c_int, [_P, _S, _S, _S]),
         "hbrbc_pairing_workspace_size": (_S, [_S]),
+        "hbrbc_g2_prepared_size": (_S, [_S]),
+        "hbrbc_g2_prepare": (ctypes.c_int, [_P, _S, _P, _P]),
+        "hbrbc_pairing_check_prepared": (ctypes.c_int, [_P, _P, _S, _P, _P, _S, _P, _P, _P]),
         "hbrbc_pairing_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P, _P]),
         "hbrbc_pairing_check_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P]),
         "hbrbc_pairing_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,

@@ -226,6 +226,13 @@ hipError_t launch_pairing_miller(const uint8_t *g1, size_t g1_stride, const uint
                                  uint8_t *status, hipStream_t s);
 hipError_t launch_pairing_miller2(const uint8_t *g1, const uint8_t *g2, size_t count,
                                   uint32_t *ws, uint8_t *status, hipStream_t s);
+size_t pairing_prepared_words(size_t points);
+hipError_t launch_g2_prepare(const uint8_t *g2, size_t count, uint32_t *prep, uint8_t *pst,
+                             hipStream_t s);
+hipError_t launch_pairing_miller_prepared(const uint8_t *g1, const uint32_t *prep,
+                                          const uint8_t *pst, const uint32_t *ib,
+                                          const uint32_t *id, size_t points, size_t count,
+                                          uint32_t *ws, uint8_t *status, hipStream_t s);
 hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_out, int per_out,
                                 const uint8_t *status, uint8_t *gt_out, uint8_t *ok_out,
                                 hipStream_t s);

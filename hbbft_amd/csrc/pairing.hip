@@ -516,10 +516,11 @@ NOINL void fp12_exp_by_x(Fp12 &r, const Fp12 &a, int shift) {
 // ---------------------------------------------------------------- Miller loop
 struct G2Proj { Fp2 x, y, z; };
 
-// T <- 2T; line tangent at T evaluated at P = (xp, yp), scaled by 2YZ^2:
-// (3X^3 - 2Y^2 Z) + (-3X^2 Z xp) v + (2 Y Z^2 yp) v w
-NOINL void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
-    Fp2 xx, w, s, ss, sss, rr, RR, B, h, t, l0, l1, l4;
+// T <- 2T and the tangent line at T before it is evaluated at P, scaled by
+// 2YZ^2: L0 + (L1 xp) v + (L4 yp) v w with L0 = 3X^3 - 2Y^2 Z, L1 = -3X^2 Z,
+// L4 = 2 Y Z^2.
+DEV void g2_dbl_line(G2Proj &T, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
+    Fp2 xx, w, s, ss, sss, rr, RR, B, h, t;
     fp2_sqr_in(xx, T.x);
     fp2_dbl(w, xx);
     fp2_add(w, w, xx);            // w = 3 X^2
@@ -527,7 +528,7 @@ NOINL void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
     fp2_dbl(s, s);                // s = 2 Y Z
     fp2_sqr_in(ss, s);
     fp2_mul_in(sss, s, ss);
-    fp2_mul_in(rr, T.y, s);          // R = Y s = 2 Y^2 Z
+    fp2_mul_in(rr, T.y, s);       // R = Y s = 2 Y^2 Z
     fp2_sqr_in(RR, rr);
     fp2_add(B, T.x, rr);
     fp2_sqr_in(B, B);
@@ -536,10 +537,8 @@ NOINL void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
     fp2_mul_in(l0, T.x, w);
     fp2_sub(l0, l0, rr);          // 3X^3 - 2Y^2 Z
     fp2_mul_in(l1, w, T.z);
-    fp2_mul_fp(l1, l1, xp);
-    fp2_neg(l1, l1);              // -3X^2 Z xp
-    fp2_mul_in(l4, s, T.z);
-    fp2_mul_fp(l4, l4, yp);       // 2 Y Z^2 yp
+    fp2_neg(l1, l1);              // -3X^2 Z
+    fp2_mul_in(l4, s, T.z);       // 2 Y Z^2
     fp2_sqr_in(h, w);
     fp2_sub(h, h, B);
     fp2_sub(h, h, B);             // h = w^2 - 2B
@@ -549,14 +548,13 @@ NOINL void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
     fp2_dbl(RR, RR);
     fp2_sub(T.y, t, RR);          // w (B - h) - 2 R^2
     T.z = sss;
-    fp12_mul_by_014(f, l0, l1, l4);
 }
 
-// T <- T + Q (Q affine); line through T and Q at P, scaled by (xq Z - X):
-// (u xq - v yq) + (-u xp) v + (v yp) v w,  u = yq Z - Y, v = xq Z - X
-NOINL void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp &xp,
-                    const Fp &yp) {
-    Fp2 u, v, uu, vv, vvv, R, A, t, l0, l1, l4;
+// T <- T + Q (Q affine) and the line through T and Q before evaluation at P,
+// scaled by (xq Z - X): L0 = u xq - v yq, L1 = -u, L4 = v with u = yq Z - Y,
+// v = xq Z - X.
+DEV void g2_add_line(G2Proj &T, const Fp2 &xq, const Fp2 &yq, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
+    Fp2 u, v, uu, vv, vvv, R, A, t;
     fp2_mul_in(u, yq, T.z);
     fp2_sub(u, u, T.y);
     fp2_mul_in(v, xq, T.z);
@@ -564,9 +562,8 @@ NOINL void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp
     fp2_mul_in(l0, u, xq);
     fp2_mul_in(t, v, yq);
     fp2_sub(l0, l0, t);
-    fp2_mul_fp(l1, u, xp);
-    fp2_neg(l1, l1);
-    fp2_mul_fp(l4, v, yp);
+    fp2_neg(l1, u);
+    l4 = v;
     fp2_sqr_in(uu, u);
     fp2_sqr_in(vv, v);
     fp2_mul_in(vvv, v, vv);
@@ -581,8 +578,29 @@ NOINL void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp
     fp2_mul_in(vvv, vvv, T.y);
     fp2_sub(T.y, t, vvv);
     fp2_mul_in(T.z, T.z, vv);
-    fp2_mul_in(T.z, T.z, v);         // Z vvv
-    fp12_mul_by_014(f, l0, l1, l4);
+    fp2_mul_in(T.z, T.z, v);      // Z vvv
+}
+
+// f <- f * line(P): the line evaluated at P = (xp, yp) (sparse (c0, c1, c4))
+DEV void apply_line(Fp12 &f, const Fp2 &l0, const Fp2 &l1, const Fp2 &l4, const Fp &xp,
+                    const Fp &yp) {
+    Fp2 a, b;
+    fp2_mul_fp(a, l1, xp);
+    fp2_mul_fp(b, l4, yp);
+    fp12_mul_by_014(f, l0, a, b);
+}
+
+NOINL void miller_dbl(G2Proj &T, Fp12 &f, const Fp &xp, const Fp &yp) {
+    Fp2 l0, l1, l4;
+    g2_dbl_line(T, l0, l1, l4);
+    apply_line(f, l0, l1, l4, xp, yp);
+}
+
+NOINL void miller_add(G2Proj &T, Fp12 &f, const Fp2 &xq, const Fp2 &yq, const Fp &xp,
+                      const Fp &yp) {
+    Fp2 l0, l1, l4;
+    g2_add_line(T, xq, yq, l0, l1, l4);
+    apply_line(f, l0, l1, l4, xp, yp);
 }
 
 // ---------------------------------------------------------------- encodings
@@ -765,6 +783,122 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4
     store_f12(ws, count, i, f);
 }
 
+// ---------------------------------------------------------------- prepared G2
+// G2 points prepared once (the crate's G2Prepared): the 68 lines of the Miller
+// loop over |x| (63 doublings, 5 additions) before evaluation at P, so every
+// check against the same G2 point (hbbft: all N shares of a ciphertext share
+// H and W) skips the twist arithmetic.  Table: point q, line s at
+// prep + (q * kLines + s) * kLineWords words: L0, L1, L4 (Fp2, Montgomery).
+constexpr int kLines = 68;
+constexpr int kLineWords = 6 * NL;
+
+DEV void store_line(uint32_t *dst, const Fp2 &l0, const Fp2 &l1, const Fp2 &l4) {
+    const Fp *v[6] = {&l0.c0, &l0.c1, &l1.c0, &l1.c1, &l4.c0, &l4.c1};
+#pragma unroll
+    for (int e = 0; e < 6; ++e)
+#pragma unroll
+        for (int w = 0; w < NL; w += 4)
+            *reinterpret_cast<uint4 *>(dst + e * NL + w) =
+                make_uint4(v[e]->l[w], v[e]->l[w + 1], v[e]->l[w + 2], v[e]->l[w + 3]);
+}
+
+DEV void load_line(const uint32_t *src, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
+    Fp *v[6] = {&l0.c0, &l0.c1, &l1.c0, &l1.c1, &l4.c0, &l4.c1};
+#pragma unroll
+    for (int e = 0; e < 6; ++e)
+#pragma unroll
+        for (int w = 0; w < NL; w += 4) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(src + e * NL + w);
+            v[e]->l[w] = q.x;
+            v[e]->l[w + 1] = q.y;
+            v[e]->l[w + 2] = q.z;
+            v[e]->l[w + 3] = q.w;
+        }
+}
+
+// One lane per G2 point: its 68 lines, and its status (0 ok, 1 infinity,
+// 2 invalid) at pst[q].
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void g2_prepare_kernel(
+    const uint8_t *__restrict__ g2, size_t count, uint32_t *__restrict__ prep,
+    uint8_t *__restrict__ pst) {
+    const size_t q = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    if (q >= count) return;
+    Fp2 xq, yq;
+    const int st = decode_g2(g2 + q * 192, xq, yq);
+    pst[q] = (uint8_t)st;
+    if (st != PT_OK) return;
+    G2Proj T;
+    T.x = xq;
+    T.y = yq;
+    fp_set(T.z.c0, kOne);
+    fp_zero(T.z.c1);
+    uint32_t *dst = prep + q * (size_t)kLines * kLineWords;
+    Fp2 l0, l1, l4;
+    for (int b = 62; b >= 0; --b) {
+        g2_dbl_line(T, l0, l1, l4);
+        store_line(dst, l0, l1, l4);
+        dst += kLineWords;
+        if ((kXAbs >> b) & 1u) {
+            g2_add_line(T, xq, yq, l0, l1, l4);
+            store_line(dst, l0, l1, l4);
+            dst += kLineWords;
+        }
+    }
+}
+
+NOINL void apply_prepared(Fp12 &f, const uint32_t *line, const Fp &xp, const Fp &yp) {
+    Fp2 l0, l1, l4;
+    load_line(line, l0, l1, l4);
+    apply_line(f, l0, l1, l4, xp, yp);
+}
+
+// One lane per check e(a, b) == e(c, d) with b, d prepared (points ib[i],
+// id[i] of the table): g1 holds a, c at rows 2i, 2i+1.  Lanes of a wave
+// checking against the same points read the same lines (one cache line
+// serves the wave).
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void miller_prepared_kernel(
+    const uint8_t *__restrict__ g1, const uint32_t *__restrict__ prep,
+    const uint8_t *__restrict__ pst, const uint32_t *__restrict__ ib,
+    const uint32_t *__restrict__ id, size_t points, size_t count, uint32_t *__restrict__ ws,
+    uint8_t *__restrict__ status) {
+    const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    if (i >= count) return;
+    Fp xa, ya, xc, yc;
+    const int sa = decode_g1(g1 + (2 * i) * 96, xa, ya);
+    const int sc = decode_g1(g1 + (2 * i + 1) * 96, xc, yc);
+    uint32_t qb = ib[i], qd = id[i];
+    // an index past the table is an invalid input, never an out-of-bounds read
+    const bool range_ok = qb < points && qd < points;
+    if (!range_ok) qb = qd = 0;
+    const int sb = range_ok ? pst[qb] : PT_BAD, sd = range_ok ? pst[qd] : PT_BAD;
+    const bool bad = sa == PT_BAD || sb == PT_BAD || sc == PT_BAD || sd == PT_BAD;
+    const bool on1 = !bad && sa == PT_OK && sb == PT_OK;
+    const bool on2 = !bad && sc == PT_OK && sd == PT_OK;
+    Fp12 f;
+    fp12_one(f);
+    if (on1 || on2) {
+        fp_neg(yc, yc);   // e(-c, d) = e(c, d)^-1
+        const uint32_t *p1 = prep + (size_t)qb * kLines * kLineWords;
+        const uint32_t *p2 = prep + (size_t)qd * kLines * kLineWords;
+        for (int b = 62; b >= 0; --b) {
+            fp12_sqr(f, f);
+            if (on1) apply_prepared(f, p1, xa, ya);
+            if (on2) apply_prepared(f, p2, xc, yc);
+            p1 += kLineWords;
+            p2 += kLineWords;
+            if ((kXAbs >> b) & 1u) {
+                if (on1) apply_prepared(f, p1, xa, ya);
+                if (on2) apply_prepared(f, p2, xc, yc);
+                p1 += kLineWords;
+                p2 += kLineWords;
+            }
+        }
+        fp12_conj(f, f);
+    }
+    status[i] = bad ? PT_BAD : PT_OK;
+    store_f12(ws, count, i, f);
+}
+
 // The crate's final exponentiation (Bls12::final_exponentiation): easy part
 // f^((p^6 - 1)(p^2 + 1)), then the hard-part chain.
 DEV void final_exp(Fp12 &out, const Fp12 &f) {
@@ -864,6 +998,29 @@ hipError_t launch_pairing_miller2(const uint8_t *g1, const uint8_t *g2, size_t c
     const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
     hipLaunchKernelGGL(miller2_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, g2, count, ws,
                        status);
+    return hipGetLastError();
+}
+
+size_t pairing_prepared_words(size_t points) { return points * (size_t)kLines * kLineWords; }
+
+hipError_t launch_g2_prepare(const uint8_t *g2, size_t count, uint32_t *prep, uint8_t *pst,
+                             hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(g2_prepare_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g2, count, prep,
+                       pst);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairing_miller_prepared(const uint8_t *g1, const uint32_t *prep,
+                                          const uint8_t *pst, const uint32_t *ib,
+                                          const uint32_t *id, size_t points, size_t count,
+                                          uint32_t *ws, uint8_t *status, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (points == 0) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(miller_prepared_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, prep, pst,
+                       ib, id, points, count, ws, status);
     return hipGetLastError();
 }
 

@@ -88,6 +88,75 @@ def pairing_check_batch(g1, g2, ws=None, stream=None):
     return ok
 
 
+def g2_prepare(g2, stream=None):
+    """Prepare G2 points (uint8 [n, 192]) once: the Miller-loop lines every
+    check against them reuses (the crate's G2Prepared).  Returns the device
+    table (uint8) for pairing_check_prepared."""
+    torch = _torch()
+    n = g2.shape[0]
+    assert g2.shape == (n, G2_BYTES) and g2.is_contiguous()
+    prep = torch.empty(max(1, lib().hbrbc_g2_prepared_size(n)), dtype=torch.uint8,
+                       device=g2.device)
+    _check(lib().hbrbc_g2_prepare(g2.data_ptr(), n, prep.data_ptr(), _stream(g2.device, stream)))
+    return prep
+
+
+def pairing_check_prepared(g1, prep, points, idx_b, idx_d, ws=None, stream=None):
+    """count checks e(a_i, P[idx_b[i]]) == e(c_i, P[idx_d[i]]) against `points`
+    prepared G2 points: g1 uint8 [2 count, 96] = a_0, c_0, ...; idx_* int32
+    [count].  Returns uint8 [count]: 1 equal, 0 not, 2 invalid point."""
+    torch = _torch()
+    n2 = g1.shape[0]
+    count = n2 // 2
+    assert n2 % 2 == 0 and g1.shape == (n2, G1_BYTES) and g1.is_contiguous()
+    assert idx_b.shape == (count,) and idx_d.shape == (count,)
+    assert idx_b.dtype == torch.int32 and idx_d.dtype == torch.int32
+    assert idx_b.is_contiguous() and idx_d.is_contiguous()
+    # an index outside [0, points) makes that check's outcome 2 (invalid) on the device
+    ok = torch.empty((count,), dtype=torch.uint8, device=g1.device)
+    if ws is None:
+        ws = workspace(count, g1.device.index)
+    assert ws.numel() >= lib().hbrbc_pairing_workspace_size(count)
+    _check(lib().hbrbc_pairing_check_prepared(g1.data_ptr(), prep.data_ptr(), points,
+                                              idx_b.data_ptr(), idx_d.data_ptr(), count,
+                                              ok.data_ptr(), ws.data_ptr(),
+                                              _stream(g1.device, stream)))
+    return ok
+
+
+def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
+    """`verify_decryption_share` for many shares of a few ciphertexts, as
+    ThresholdDecrypt receives them: ciphertexts = [(hash G2, W G2)], shares =
+    [(ciphertext index, share G1, pk_share G1)].  Each ciphertext's H and W
+    are prepared once; shares are grouped by ciphertext so a wave shares its
+    lines.  Returns bools in the order of `shares`."""
+    import numpy as np
+    torch = _torch()
+    if not shares:
+        return []
+    dev = "cuda:%d" % device
+    g2 = np.empty((2 * len(ciphertexts), G2_BYTES), np.uint8)
+    for j, (h, w) in enumerate(ciphertexts):
+        g2[2 * j] = np.frombuffer(h, np.uint8)
+        g2[2 * j + 1] = np.frombuffer(w, np.uint8)
+    prep = g2_prepare(torch.from_numpy(g2).to(dev))
+    order = sorted(range(len(shares)), key=lambda i: shares[i][0])
+    g1 = np.empty((2 * len(shares), G1_BYTES), np.uint8)
+    ib = np.empty(len(shares), np.int32)
+    for r, i in enumerate(order):
+        ct, share, pk = shares[i]
+        g1[2 * r] = np.frombuffer(share, np.uint8)
+        g1[2 * r + 1] = np.frombuffer(pk, np.uint8)
+        ib[r] = 2 * ct
+    ok = pairing_check_prepared(torch.from_numpy(g1).to(dev), prep, 2 * len(ciphertexts),
+                                torch.from_numpy(ib).to(dev), torch.from_numpy(ib + 1).to(dev))
+    okh = ok.cpu().tolist()
+    out = [False] * len(shares)
+    for r, i in enumerate(order):
+        out[i] = okh[r] == CHECK_OK
+    return out
+
+
 def pairing_check(a, b, c, d):
     """Per-call shim: e(a, b) == e(c, d) for host byte strings (one device
     round trip).  Raises RseError(InvalidArgument) on an invalid point."""

@@ -424,6 +424,22 @@ int hbrbc_pairing_batch(const uint8_t *g1, const uint8_t *g2, size_t count, uint
  * workspace >= hbrbc_pairing_workspace_size(2 count).  Device memory, async. */
 int hbrbc_pairing_check_batch(const uint8_t *g1, const uint8_t *g2, size_t count,
                               uint8_t *ok_out, void *workspace, void *stream);
+/* Prepared G2 points (the crate's G2Prepared): the 68 Miller-loop lines of
+ * each point, computed once and shared by every check against it (hbbft:
+ * the N decryption shares of a ciphertext are all checked against its H and
+ * W).  `prepared` >= hbrbc_g2_prepared_size(count) bytes of device memory;
+ * an invalid point is marked there and fails every check that uses it. */
+size_t hbrbc_g2_prepared_size(size_t points);
+int hbrbc_g2_prepare(const uint8_t *g2, size_t count, void *prepared, void *stream);
+/* count checks e(a_i, P[idx_b[i]]) == e(c_i, P[idx_d[i]]) against prepared
+ * points P (`points` of them in `prepared`): g1 holds a_0, c_0, a_1, c_1, ...;
+ * ok_out as hbrbc_pairing_check_batch (an index >= points makes that check 2).
+ * Checks that share prepared points
+ * should be adjacent (a wave then reads each line once).  workspace >=
+ * hbrbc_pairing_workspace_size(count).  Device memory, async on `stream`. */
+int hbrbc_pairing_check_prepared(const uint8_t *g1, const void *prepared, size_t points,
+                                 const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
+                                 uint8_t *ok_out, void *workspace, void *stream);
 /* Per-call shim on host memory (one check, synchronous, current device):
  * *result = 1 if e(a, b) == e(c, d), 0 if not; HBRBC_E_INVALID_ARG for an
  * invalid point. */

@@ -47,8 +47,26 @@ def main():
         pool.append({"a": B.g1_bytes(share).hex(), "b": B.g2_bytes(H).hex(),
                      "c": B.g1_bytes(pk).hex(), "d": B.g2_bytes(W).hex(),
                      "expect": i % 4 != 3, "kind": "verify_decryption_share"})
+    # grouped bench pool (bench.py's f4 leg): 4 ciphertexts x 64 decryption shares,
+    # every share of a ciphertext checked against its H and W; one in eight tampered
+    groups = []
+    for g in range(4):
+        h, r_enc = rng.randrange(1, B.R), rng.randrange(1, B.R)
+        H = B.g2_mul(B.G2_GEN, h)
+        U = B.g1_mul(B.G1_GEN, r_enc)
+        W = B.g2_mul(H, r_enc)
+        sh = []
+        for s in range(64):
+            sk = rng.randrange(1, B.R)
+            share = B.g1_mul(U, sk)
+            good = (s + g) % 8 != 7
+            if not good:
+                share = B.g1_add(share, B.G1_GEN)
+            sh.append({"share": B.g1_bytes(share).hex(),
+                       "pk": B.g1_bytes(B.g1_mul(B.G1_GEN, sk)).hex(), "expect": good})
+        groups.append({"hash": B.g2_bytes(H).hex(), "w": B.g2_bytes(W).hex(), "shares": sh})
     out = {"source": "oracle/bls_oracle.py (restatement of the pairing crate's BLS12-381)",
-           "pairings": vectors, "checks": checks, "bench_pool": pool}
+           "pairings": vectors, "checks": checks, "bench_pool": pool, "bench_groups": groups}
     path = os.path.join(ROOT, "tests", "golden", "bls_vectors.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)

@@ -153,3 +153,51 @@ def test_pairing_batch_at_size_vs_c_restatement():
     ref_gt, ref_st = bls_c.pairing_batch(g1b, g2b, 4096, min(16, os.cpu_count() or 1))
     assert st.cpu().numpy().tobytes() == ref_st == b"\0" * 4096
     assert gt.cpu().numpy().tobytes() == ref_gt
+
+
+def test_prepared_checks_match_plain_checks():
+    """Checks against prepared G2 points (the crate's G2Prepared, shared by all
+    shares of a ciphertext) give exactly the outcomes of the plain checks:
+    valid and tampered shares, several ciphertexts, infinity and invalid
+    points, and the grouped verify_decryption_shares helper."""
+    from hbbft_amd import threshold as T
+    rng = random.Random(21)
+    cts, shares, expect = [], [], []
+    for j in range(3):
+        h, r_enc = rng.randrange(1, B.R), rng.randrange(1, B.R)
+        H = B.g2_mul(B.G2_GEN, h)
+        U = B.g1_mul(B.G1_GEN, r_enc)
+        W = B.g2_mul(H, r_enc)
+        cts.append((B.g2_bytes(H), B.g2_bytes(W)))
+        for s in range(5):
+            sk = rng.randrange(1, B.R)
+            share = B.g1_mul(U, sk)
+            good = (s + j) % 3 != 0
+            if not good:
+                share = B.g1_add(share, B.G1_GEN)
+            shares.append((j, B.g1_bytes(share), B.g1_bytes(B.g1_mul(B.G1_GEN, sk))))
+            expect.append(good)
+    # interleave the ciphertexts so grouping has work to do
+    perm = list(range(len(shares)))
+    rng.shuffle(perm)
+    shares = [shares[i] for i in perm]
+    expect = [expect[i] for i in perm]
+    assert T.verify_decryption_shares_grouped(cts, shares) == expect
+    plain = T.verify_decryption_shares([(s, pk, cts[j][0], cts[j][1]) for j, s, pk in shares])
+    assert plain == expect
+    # infinity / invalid prepared points and G1 points
+    bad2 = bytearray(B.g2_bytes(B.G2_GEN))
+    bad2[-1] ^= 1
+    g2 = _t([B.g2_bytes(B.G2_GEN), B.g2_bytes(None), bytes(bad2)], 192)
+    prep = T.g2_prepare(g2)
+    P = B.g1_bytes(B.g1_mul(B.G1_GEN, 7))
+    inf1 = B.g1_bytes(None)
+    import torch
+    g1 = _t([P, P, inf1, P, P, inf1, P, P], 96)
+    ib = torch.tensor([0, 1, 0, 2], dtype=torch.int32, device="cuda:0")
+    idd = torch.tensor([0, 0, 0, 0], dtype=torch.int32, device="cuda:0")
+    # e(P,G)==e(P,G): 1;  e(inf,..)=1 vs e(P,G) != 1: 0;  e(P,G) vs e(inf,G)=1: 0;  invalid: 2
+    assert T.pairing_check_prepared(g1, prep, 3, ib, idd).cpu().tolist() == [1, 0, 0, 2]
+    # indices past the table (as uint32: -1 is 2^32-1) are invalid inputs, not reads
+    ib2 = torch.tensor([0, 3, -1, 0], dtype=torch.int32, device="cuda:0")
+    assert T.pairing_check_prepared(g1, prep, 3, ib2, idd).cpu().tolist() == [1, 2, 2, 1]

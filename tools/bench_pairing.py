@@ -19,7 +19,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=16384)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--prepared", action="store_true",
+                    help="grouped checks against prepared G2 points (64 shares per ciphertext)")
     a = ap.parse_args()
+    if a.prepared:
+        return prepared(a)
     import numpy as np
     import torch
     from oracle import bls_oracle as B
@@ -57,6 +61,49 @@ def main():
     print(json.dumps({"n_checks": a.n, "waves": os.environ.get("HBRBC_PAIR_WAVES", "default"),
                       "ms": t * 1e3, "checks_per_s": a.n / t, "pairings_per_s": 2 * a.n / t,
                       "outcomes_exact": True}), flush=True)
+
+
+def prepared(a):
+    """a.n checks in groups of 64 shares per ciphertext (the fixture groups of
+    tests/golden/bls_vectors.json tiled): each step prepares the H and W of
+    every group (inside the timing) and checks its shares against them."""
+    import numpy as np
+    import torch
+    from hbbft_amd import threshold as T
+    groups = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))["bench_groups"]
+    ng = a.n // 64
+    g2 = np.empty((2 * ng, 192), np.uint8)
+    g1 = np.empty((2 * a.n, 96), np.uint8)
+    expect = []
+    for q in range(ng):
+        grp = groups[q % len(groups)]
+        g2[2 * q] = np.frombuffer(bytes.fromhex(grp["hash"]), np.uint8)
+        g2[2 * q + 1] = np.frombuffer(bytes.fromhex(grp["w"]), np.uint8)
+        for s, sh in enumerate(grp["shares"]):
+            i = q * 64 + s
+            g1[2 * i] = np.frombuffer(bytes.fromhex(sh["share"]), np.uint8)
+            g1[2 * i + 1] = np.frombuffer(bytes.fromhex(sh["pk"]), np.uint8)
+            expect.append(1 if sh["expect"] else 0)
+    d1, d2 = torch.from_numpy(g1).cuda(), torch.from_numpy(g2).cuda()
+    ib = torch.arange(a.n, dtype=torch.int32, device="cuda") // 64 * 2
+    idd = ib + 1
+    ws = T.workspace(a.n)
+
+    def run():
+        prep = T.g2_prepare(d2)
+        return T.pairing_check_prepared(d1, prep, 2 * ng, ib, idd, ws)
+    ok = run()
+    torch.cuda.synchronize()
+    assert ok.cpu().tolist() == expect, "check outcomes differ from the fixtures"
+    times = []
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    print(json.dumps({"n_checks": a.n, "mode": "prepared", "groups": ng, "ms": t * 1e3,
+                      "checks_per_s": a.n / t, "outcomes_exact": True}), flush=True)
 
 
 if __name__ == "__main__":

@@ -16,7 +16,8 @@ def main():
     for f in glob.glob(d + "/pmc/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             k = row.get("Kernel_Name", "")
-            kern = "miller" if "miller" in k else "final_exp" if "final_exp_kernel" in k else None
+            kern = ("prepare" if "g2_prepare" in k else "miller" if "miller" in k
+                    else "final_exp" if "final_exp_kernel" in k else None)
             if kern:
                 vals[kern][row["Counter_Name"]].append(float(row["Counter_Value"]))
     per = {}
@@ -27,7 +28,8 @@ def main():
     for f in glob.glob(d + "/trace/**/*kernel_stats.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             k = row["Name"]
-            kern = "miller" if "miller" in k else "final_exp" if "final_exp_kernel" in k else None
+            kern = ("prepare" if "g2_prepare" in k else "miller" if "miller" in k
+                    else "final_exp" if "final_exp_kernel" in k else None)
             if kern:
                 stats[kern] = float(row["AverageNs"]) / 1e6
     ops = {k: v["SQ_INSTS_VALU"] * 64 / n for k, v in per.items() if "SQ_INSTS_VALU" in v}
