@@ -519,7 +519,7 @@ struct G2Proj { Fp2 x, y, z; };
 // T <- 2T and the tangent line at T before it is evaluated at P, scaled by
 // 2YZ^2: L0 + (L1 xp) v + (L4 yp) v w with L0 = 3X^3 - 2Y^2 Z, L1 = -3X^2 Z,
 // L4 = 2 Y Z^2.
-DEV void g2_dbl_line(G2Proj &T, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
+NOINL void g2_dbl_line(G2Proj &T, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
     Fp2 xx, w, s, ss, sss, rr, RR, B, h, t;
     fp2_sqr_in(xx, T.x);
     fp2_dbl(w, xx);
@@ -553,7 +553,7 @@ DEV void g2_dbl_line(G2Proj &T, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
 // T <- T + Q (Q affine) and the line through T and Q before evaluation at P,
 // scaled by (xq Z - X): L0 = u xq - v yq, L1 = -u, L4 = v with u = yq Z - Y,
 // v = xq Z - X.
-DEV void g2_add_line(G2Proj &T, const Fp2 &xq, const Fp2 &yq, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
+NOINL void g2_add_line(G2Proj &T, const Fp2 &xq, const Fp2 &yq, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
     Fp2 u, v, uu, vv, vvv, R, A, t;
     fp2_mul_in(u, yq, T.z);
     fp2_sub(u, u, T.y);
