@@ -467,8 +467,9 @@ hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, X
 // Fused unframe (decode paths): the generic reconstruct kernel writes the
 // payload bytes of the data rows it reads or rebuilds, so unframe's re-read of
 // k*S bytes per instance disappears (decode_check + a zero-fill fixup remain).
-// Needs S % 4 == 0 (dword-aligned destinations) and no pattern-specialised
-// decoder in the call; HBRBC_UNFRAME_FUSED=0 keeps the separate unframe (A/B).
+// Needs S % 4 == 0 (dword-aligned destinations); the pattern-specialised
+// decoders (v17 code objects) write the payload the same way.
+// HBRBC_UNFRAME_FUSED=0 keeps the separate unframe (A/B).
 bool unframe_fusable(const hbrbc_ctx *c, size_t shard_len, size_t payload_stride) {
     const char *e = getenv("HBRBC_UNFRAME_FUSED");
     if (e && !std::strcmp(e, "0")) return false;
@@ -522,6 +523,12 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
         x.slot_hash = reinterpret_cast<const unsigned long *>(c->pc_hash.as<uint64_t>());
         x.hash_slots = c->pc_cap;
         x.p_only = -1;
+        x.S = (unsigned)shard_len;
+        if (uf_payload) {   // fused unframe in the pattern decoders too
+            x.uf_payload = uf_payload;
+            x.uf_stride = uf_stride;
+            x.uf_status = status;
+        }
         for (const auto &g : ds->second.groups)
             HB_HIP(launch_xor_group(g, false, ds->second.rt, x, count, s));
     }
@@ -547,7 +554,7 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
     g.rt = c->rt_rec;
     g.mode = c->gf_mode;
     g.count = count;
-    if (uf_payload && !spec) {
+    if (uf_payload) {
         g.payload = uf_payload;
         g.payload_stride = uf_stride;
         g.payload_S = (uint32_t)shard_len;
@@ -575,7 +582,7 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v16.co";
+           "_v17.co";   // v17: fused-unframe arguments
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
@@ -691,6 +698,8 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
         p.depth = depth;
         p.rb = rb;
         p.guard = hash;
+        p.uf_k = (int)k;            // fused unframe: rebuilt data rows, and
+        p.uf_inputs = gi == 0;      // the present ones from the first program
         out.push_back(std::move(p));
     }
     return true;
@@ -770,7 +779,8 @@ hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, X
     void *args[] = {&a.base,     &a.inst_stride, &a.shard_stride, &a.block_stride,
                     &a.row_bytes, &a.waves_per_row, &a.payloads,  &a.payload_stride,
                     &a.P,        &a.S,           &a.pat,          &a.slot_hash,
-                    &a.hash_slots, &a.p_only};
+                    &a.hash_slots, &a.p_only,     &a.uf_payload,   &a.uf_stride,
+                    &a.uf_status};
     hipFunction_t fn = fused ? g.fe : g.fn;
     if (!spec_pass_split()) {
         a.p_only = -1;
@@ -1898,7 +1908,8 @@ int hbrbc_unframe_fused(const hbrbc_ctx *c, size_t shard_len, size_t payload_str
     if (rows_per_block && rows_per_block < c->n) rows.rb = (uint32_t)rows_per_block;
     const auto ds = c->dec_spec.find(code_rb(rows));
     const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
-    return unframe_fusable(c, shard_len, payload_stride) && !spec ? 1 : 0;
+    (void)spec;   // pattern decoders unframe too (v17 code objects)
+    return unframe_fusable(c, shard_len, payload_stride) ? 1 : 0;
 }
 
 // ---- threshold-decrypt share verification (pairing.hip) ----

@@ -27,7 +27,7 @@
 // (tests compare both with the oracle).
 //
 // Code objects are cached as files under <lib dir>/jit (names from
-// encode_kernel_name / decode_kernel_name + "_v16.co");
+// encode_kernel_name / decode_kernel_name + "_v17.co");
 // __graft_entry__.build() pre-generates the encoders of the BASELINE
 // validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
@@ -95,6 +95,22 @@ __device__ __forceinline__ void hb_frame_head(const u32x4 q0, const u32x4 q1, un
 __device__ __forceinline__ void hb_frame_head2(const u32x4 qa, unsigned P, unsigned lb, uint32_t (&x)[8]) {
     const uint32_t w[5] = {__builtin_bswap32(P), qa[0], qa[1], qa[2], qa[3]};
     _Pragma("unroll") for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], lb);
+}
+// Fused unframe: 16 bytes of data row `row` at byte `pos` are payload bytes
+// row*S + pos - 4 .. +15 (S % 4 == 0: dword-aligned; the 4-byte length prefix
+// and the row padding are not payload) -- kernels.hip unframe_put.
+typedef unsigned int hb_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void hb_uf_put(uint8_t *pb, unsigned S, unsigned row, unsigned pos,
+                                          uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if (pos >= S) return;
+    const long dst = (long)row * S + pos - 4;
+    if (dst >= 0 && pos + 16u <= S) {
+        *reinterpret_cast<hb_u32x4_a4 *>(pb + dst) = (hb_u32x4_a4){a, b, c, d};
+        return;
+    }
+    const uint32_t w[4] = {a, b, c, d};
+    _Pragma("unroll") for (int q = 0; q < 4; ++q)
+        if (pos + 4u * q < S && dst + 4 * q >= 0) *reinterpret_cast<uint32_t *>(pb + dst + 4 * q) = w[q];
 }
 // 8x32 bit transpose of 8 dwords (three delta swaps; an involution)
 __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {
@@ -258,7 +274,8 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
          "    unsigned long block_stride, unsigned row_bytes, unsigned waves_per_row,\n"
          "    const uint8_t *__restrict__ payloads, unsigned long payload_stride, unsigned P, unsigned S,\n"
          "    const int *__restrict__ pat, const unsigned long *__restrict__ slot_hash, int hash_slots,\n"
-         "    int p_only) {\n"
+         "    int p_only, uint8_t *__restrict__ uf_payload, unsigned long uf_stride,\n"
+         "    const int *__restrict__ uf_status) {\n"
          "  const unsigned long inst = blockIdx.x / waves_per_row;\n";
     if (p.guard) {
         // reconstruct of one cached erasure pattern: other patterns return
@@ -284,6 +301,9 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
          // the row offset (row % rb) * shard_stride in an SGPR (soffset) and
          // the lane offset in one VGPR -- no per-lane 64-bit address per row
          "  uint8_t *const ib = base + inst * inst_stride;\n";
+    if (p.uf_k > 0)
+        o << "  uint8_t *const ufp = (uf_payload && uf_status[inst] == 0) ? uf_payload + inst * uf_stride"
+             " : (uint8_t *)0;\n";
     for (int q : blocks)
         o << "  const __amdgpu_buffer_rsrc_t rs" << q << " = __builtin_amdgcn_make_buffer_rsrc(ib"
           << (q ? " + " + std::to_string(q) + "ul * block_stride" : std::string()) << ", (short)0, "
@@ -405,7 +425,12 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
                 const std::string lc = "l[" + std::to_string(cur) + "]";
                 o << "      { const u32x4 hh = full ? h[" << cur << "] : (u32x4)(0u);\n"
                   << "        uint32_t x[8] = {" << lc << "[0], " << lc << "[1], " << lc << "[2], " << lc
-                  << "[3], hh[0], hh[1], hh[2], hh[3]};\n        hb_tr(x);\n";
+                  << "[3], hh[0], hh[1], hh[2], hh[3]};\n";
+                if (p.uf_k > 0 && p.uf_inputs && ps == 0 && row < p.uf_k)
+                    o << "        if (ufp && active) { hb_uf_put(ufp, S, " << row
+                      << "u, off, x[0], x[1], x[2], x[3]); if (full) hb_uf_put(ufp, S, " << row
+                      << "u, off2, x[4], x[5], x[6], x[7]); }\n";
+                o << "        hb_tr(x);\n";
             }
             if (rt <= 8)   // short passes: the nibble-subset network
                 gen_nibble_network(o, cv, t0, rows, jj);
@@ -431,6 +456,10 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
               << at << "[2], " << at << "[3]}, rs" << blk(row) << ", off, so_, HB_ST_AUX);\n"
               << "          if (full) __builtin_amdgcn_raw_buffer_store_b128((u32x4){" << at << "[4], " << at
               << "[5], " << at << "[6], " << at << "[7]}, rs" << blk(row) << ", off2, so_, HB_ST_AUX); }\n";
+            if (p.uf_k > 0 && row < p.uf_k)
+                o << "        if (ufp) { hb_uf_put(ufp, S, " << row << "u, off, " << at << "[0], " << at
+                  << "[1], " << at << "[2], " << at << "[3]); if (full) hb_uf_put(ufp, S, " << row
+                  << "u, off2, " << at << "[4], " << at << "[5], " << at << "[6], " << at << "[7]); }\n";
         }
         o << "      }\n      break; }\n";
     }

@@ -36,6 +36,11 @@ struct XorProgram {
     bool split = true;
     uint64_t guard = 0;
     bool fused = false;
+    // fused unframe (decoders): payload bytes of the data rows (< uf_k) this
+    // program rebuilds, and of its input data rows if uf_inputs (one program
+    // of a pattern writes them); 0 = none
+    int uf_k = 0;
+    bool uf_inputs = false;
 };
 
 // Kernel argument list shared by every generated kernel (hipModuleLaunchKernel).
@@ -50,6 +55,10 @@ struct XorArgs {
     const unsigned long *slot_hash;
     int hash_slots;
     int p_only;
+    // fused unframe: payload slab (nullptr = off), its stride, reconstruct status
+    uint8_t *uf_payload;
+    unsigned long uf_stride;
+    const int *uf_status;
 };
 
 // Waves per workgroup of a program with npass passes (one per pass, <= 8).

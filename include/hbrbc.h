@@ -384,8 +384,8 @@ const char *hbrbc_stage_name(int stage);
 
 /* 1 if hbrbc_decode_batch / _rows on this context (row block rows_per_block,
  * 0 = plain layout) write the payload from the reconstruct kernel (fused
- * unframe: shard_len % 4 == 0, payload_stride % 16 == 0, no
- * pattern-specialised decoder loaded, HBRBC_UNFRAME_FUSED != 0), else 0.
+ * unframe, in the generic and the pattern-specialised decoders: shard_len
+ * % 4 == 0, payload_stride % 16 == 0, HBRBC_UNFRAME_FUSED != 0), else 0.
  * Outputs are identical either way; this only tells where the bytes move. */
 int hbrbc_unframe_fused(const hbrbc_ctx *ctx, size_t shard_len, size_t payload_stride,
                         size_t rows_per_block);

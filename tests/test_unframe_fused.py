@@ -94,3 +94,46 @@ def test_fused_unframe_matches_separate_and_oracle(torch_cuda, n, plen):
     if f:
         assert st[3] == 10 and st[4] == 65
     assert plo[6] == lie or st[6] != 0
+
+
+@pytest.mark.parametrize("n,plen", [(16, 2396), (64, 20050)])
+def test_fused_unframe_in_specialised_decoder(torch_cuda, n, plen):
+    """Instances of a pattern with a specialised (JIT) decoder write their
+    payload from that decoder (first program: present data rows; every
+    program: rebuilt data rows); instances of other patterns from the generic
+    kernel.  Whole slots equal the separate unframe's and the oracle's."""
+    torch = torch_cuda
+    import hbbft_amd as hb
+    f = (n - 1) // 3
+    count = 6
+    rb = hb.RbcBatch(n, f, device=0)
+    S = hb.shard_len(plen, rb.k)
+    assert S % 4 == 0
+    pay = np.stack([orc.gen_payload(13, i, plen) for i in range(count)])
+    stride_p = (plen + 15) // 16 * 16
+    payloads = torch.zeros((count, stride_p), dtype=torch.uint8, device="cuda")
+    payloads[:, :plen] = torch.from_numpy(pay).cuda()
+    slab = rb.alloc_slab(count, S)
+    rb.frame(payloads, plen, slab)
+    rb.encode(slab, S)
+    nodes = rb.alloc_nodes(count)
+    rb.merkle(slab, S, nodes)
+    roots = nodes[:, -1, :].clone()
+    pattern = np.ones(n, np.uint8)
+    pattern[[0, 2, n - 1] + list(range(5, 5 + f - 3))] = 0      # row 0 (the length) missing
+    rb.specialise_decoder(pattern)
+    present = np.tile(pattern, (count, 1))
+    rng = np.random.default_rng(n)
+    present[4] = 1
+    present[4, rng.choice(n, f, replace=False)] = 0              # another pattern: generic
+    present[5] = 1                                               # all present
+    pres = torch.from_numpy(present).cuda()
+    a = _decode(torch, rb, slab, S, pres, roots, "1")
+    b = _decode(torch, rb, slab, S, pres, roots, "0")
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    out, plo, st = a
+    slot = (rb.k * S - 4 + 15) // 16 * 16
+    assert (st == 0).all() and (plo == plen).all()
+    for i in range(count):
+        assert out[i, :plen].tobytes() == pay[i].tobytes() and (out[i, plen:slot] == 0).all(), i
