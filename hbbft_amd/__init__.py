@@ -128,6 +128,10 @@ def lib():
         "hbrbc_jit_decode_groups": (_S, [_S, _S, _P]),
         "hbrbc_jit_build_decode": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p]),
         "hbrbc_jit_decode_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_char_p, _S]),
+        "hbrbc_jit_build_decode_variant": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_int,
+                                                          ctypes.c_char_p]),
+        "hbrbc_jit_decode_variant_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_int,
+                                                              ctypes.c_char_p, _S]),
         "hbrbc_unframe_fused": (ctypes.c_int, [_P, _S, _S, _S]),
         "hbrbc_pairing_workspace_size": (_S, [_S]),
         "hbrbc_g2_prepared_size": (_S, [_S]),
@@ -185,19 +189,22 @@ def jit_decode_groups(data_shards, parity_shards, present):
 
 
 def jit_build_decode(data_shards, parity_shards, present, group, rows_per_block=0,
-                     directory=None):
-    """Compile one group of the pattern-specialised decoder into the cache."""
+                     directory=None, fused_unframe=False):
+    """Compile one group of the pattern-specialised decoder (or of its
+    fused-unframe variant) into the cache."""
     m = _mask_buffer(present)
     d = directory.encode() if directory else None
-    _check(lib().hbrbc_jit_build_decode(data_shards, parity_shards, m.ctypes.data,
-                                        rows_per_block, group, d))
+    _check(lib().hbrbc_jit_build_decode_variant(data_shards, parity_shards, m.ctypes.data,
+                                                rows_per_block, group, int(fused_unframe), d))
 
 
-def jit_decode_file_name(data_shards, parity_shards, present, group=0, rows_per_block=0):
+def jit_decode_file_name(data_shards, parity_shards, present, group=0, rows_per_block=0,
+                         fused_unframe=False):
     m = _mask_buffer(present)
     buf = ctypes.create_string_buffer(256)
-    _check(lib().hbrbc_jit_decode_file_name(data_shards, parity_shards, m.ctypes.data,
-                                            rows_per_block, group, buf, 256))
+    _check(lib().hbrbc_jit_decode_variant_file_name(data_shards, parity_shards, m.ctypes.data,
+                                                    rows_per_block, group, int(fused_unframe),
+                                                    buf, 256))
     return buf.value.decode()
 
 

@@ -260,6 +260,11 @@ struct hbrbc_ctx {
         uint64_t hash;
         int rt;
         std::vector<SpecGroup> groups;
+        // the fused-unframe variant of the same programs, loaded (or compiled)
+        // on the first call that fuses: 0 untried, 1 loaded, -1 unavailable
+        std::vector<SpecGroup> uf_groups;
+        int uf_state = 0;
+        std::vector<uint8_t> present;
     };
     std::map<int, DecSpec> dec_spec;
     DevBuf d_matrix, d_enc_coefs, d_enc_in, d_enc_out;
@@ -477,6 +482,39 @@ bool unframe_fusable(const hbrbc_ctx *c, size_t shard_len, size_t payload_stride
            (uint64_t)c->k * shard_len > 4;
 }
 
+bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const uint8_t *present,
+                     int rb, std::vector<XorProgram> &out, uint64_t &hash, int &rt, bool uf);
+int load_program(const XorProgram &p, bool compile, hbrbc_ctx::SpecGroup &g);
+void drop_groups(std::vector<hbrbc_ctx::SpecGroup> &gs);
+
+// The _uf variant of a specialised decoder, loaded (or, unless HBRBC_JIT=0,
+// compiled) once; false if unavailable (the call then unframes separately).
+bool uf_decoder(hbrbc_ctx *c, hbrbc_ctx::DecSpec &d, int rb) {
+    if (d.uf_state == 0) {
+        std::vector<XorProgram> progs;
+        uint64_t hash = 0;
+        int rt = 2;
+        const char *mode = getenv("HBRBC_JIT");
+        const bool compile = !(mode && !std::strcmp(mode, "0"));
+        const std::string saved = g_err;
+        d.uf_state = -1;
+        if (decode_programs(c->matrix, c->k, c->n, d.present.data(), rb, progs, hash, rt, true)) {
+            d.uf_state = 1;
+            for (const auto &p : progs) {
+                hbrbc_ctx::SpecGroup g{0, (int)p.out_rows.size(), nullptr, nullptr, nullptr};
+                if (load_program(p, compile, g)) {
+                    drop_groups(d.uf_groups);
+                    d.uf_state = -1;
+                    break;
+                }
+                d.uf_groups.push_back(g);
+            }
+        }
+        g_err = saved;   // a missing variant is not an error of the caller's call
+    }
+    return d.uf_state == 1;
+}
+
 int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &rows,
                     size_t inst_stride, const uint8_t *present, size_t count, int32_t *status,
                     hipStream_t s, uint8_t *uf_payload = nullptr, size_t uf_stride = 0,
@@ -512,6 +550,8 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
     StageTimer t(c, HBRBC_STAGE_RECONSTRUCT, s);
     const auto ds = c->dec_spec.find(code_rb(rows));
     const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
+    // fusing with a specialised decoder needs its _uf variant
+    if (spec && uf_payload && !uf_decoder(c, ds->second, code_rb(rows))) uf_payload = nullptr;
     if (spec) {
         XorArgs x{};
         x.base = shards;
@@ -524,12 +564,12 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
         x.hash_slots = c->pc_cap;
         x.p_only = -1;
         x.S = (unsigned)shard_len;
-        if (uf_payload) {   // fused unframe in the pattern decoders too
+        if (uf_payload) {       // fused unframe in the pattern decoders too (_uf variant)
             x.uf_payload = uf_payload;
             x.uf_stride = uf_stride;
             x.uf_status = status;
         }
-        for (const auto &g : ds->second.groups)
+        for (const auto &g : uf_payload ? ds->second.uf_groups : ds->second.groups)
             HB_HIP(launch_xor_group(g, false, ds->second.rt, x, count, s));
     }
     GfApplyArgs g{};
@@ -582,7 +622,7 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v17.co";   // v17: fused-unframe arguments
+           "_v19.co";   // v19: plain decoders + _uf variants
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
@@ -675,7 +715,8 @@ XorProgram encode_program(size_t k, size_t m, const uint8_t *parity_rows, int rt
 
 // The decoder programs of one erasure pattern (output-row groups).
 bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const uint8_t *present,
-                     int rb, std::vector<XorProgram> &out, uint64_t &hash, int &rt) {
+                     int rb, std::vector<XorProgram> &out, uint64_t &hash, int &rt,
+                     bool uf = false) {
     std::vector<int> valid, missing;
     std::vector<uint8_t> rows;
     if (!recovery_rows(mat, k, n, present, valid, missing, rows)) return false;
@@ -689,7 +730,7 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
         p.sync = spec_sync();
         p.split = spec_split();
         p.name = decode_kernel_name(n, hash, rt, depth, groups[gi].first, groups[gi].second, rb,
-                                    p.sync, p.split);
+                                    p.sync, p.split) + (uf ? "_uf" : "");
         p.in_rows = valid;
         p.out_rows.assign(missing.begin() + groups[gi].first, missing.begin() + groups[gi].second);
         p.coefs.assign(rows.begin() + (size_t)groups[gi].first * k,
@@ -698,8 +739,8 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
         p.depth = depth;
         p.rb = rb;
         p.guard = hash;
-        p.uf_k = (int)k;            // fused unframe: rebuilt data rows, and
-        p.uf_inputs = gi == 0;      // the present ones from the first program
+        p.uf_k = uf ? (int)k : 0;       // fused unframe: rebuilt data rows, and
+        p.uf_inputs = uf && gi == 0;    // the present ones from the first program
         out.push_back(std::move(p));
     }
     return true;
@@ -1018,7 +1059,10 @@ void hbrbc_coding_free(hbrbc_ctx *c) {
     c->pin.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (auto &kv : c->enc_spec) drop_groups(kv.second);
-    for (auto &kv : c->dec_spec) drop_groups(kv.second.groups);
+    for (auto &kv : c->dec_spec) {
+        drop_groups(kv.second.groups);
+        drop_groups(kv.second.uf_groups);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1412,6 +1456,7 @@ int hbrbc_decoder_specialise(hbrbc_ctx *c, const uint8_t *present, size_t rows_p
     hbrbc_ctx::DecSpec d;
     d.hash = hash;
     d.rt = rt;
+    d.present.assign(present, present + c->n);
     int ng = 0;
     for (const auto &p : progs) {
         hbrbc_ctx::SpecGroup g{0, (int)p.out_rows.size(), nullptr, nullptr, nullptr};
@@ -1425,7 +1470,10 @@ int hbrbc_decoder_specialise(hbrbc_ctx *c, const uint8_t *present, size_t rows_p
     }
     HB_HIP(hipDeviceSynchronize());  // no launch of the previous decoder is in flight
     auto it = c->dec_spec.find(rb);
-    if (it != c->dec_spec.end()) drop_groups(it->second.groups);
+    if (it != c->dec_spec.end()) {
+        drop_groups(it->second.groups);
+        drop_groups(it->second.uf_groups);
+    }
     c->dec_spec[rb] = std::move(d);
     return HBRBC_OK;
 }
@@ -1442,6 +1490,13 @@ size_t hbrbc_jit_decode_groups(size_t data_shards, size_t parity_shards, const u
 
 int hbrbc_jit_build_decode(size_t data_shards, size_t parity_shards, const uint8_t *present,
                            size_t rows_per_block, size_t group, const char *dir) {
+    return hbrbc_jit_build_decode_variant(data_shards, parity_shards, present, rows_per_block,
+                                          group, 0, dir);
+}
+
+int hbrbc_jit_build_decode_variant(size_t data_shards, size_t parity_shards,
+                                   const uint8_t *present, size_t rows_per_block, size_t group,
+                                   int fused_unframe, const char *dir) {
     std::vector<uint8_t> mat;
     const size_t n = data_shards + parity_shards;
     if (!present || data_shards == 0 || n > 256)
@@ -1452,7 +1507,7 @@ int hbrbc_jit_build_decode(size_t data_shards, size_t parity_shards, const uint8
     std::vector<XorProgram> progs;
     uint64_t hash;
     int rt;
-    if (!decode_programs(mat, data_shards, n, present, rb, progs, hash, rt))
+    if (!decode_programs(mat, data_shards, n, present, rb, progs, hash, rt, fused_unframe != 0))
         return fail(HBRBC_E_INVALID_ARG, "pattern has nothing to rebuild or too few shards");
     if (group >= progs.size()) return fail(HBRBC_E_INVALID_ARG, "group %zu of %zu", group, progs.size());
     std::vector<char> code;
@@ -1836,6 +1891,14 @@ int hbrbc_jit_file_name(size_t data_shards, size_t parity_shards, size_t group, 
 
 int hbrbc_jit_decode_file_name(size_t data_shards, size_t parity_shards, const uint8_t *present,
                                size_t rows_per_block, size_t group, char *buf, size_t buf_len) {
+    return hbrbc_jit_decode_variant_file_name(data_shards, parity_shards, present, rows_per_block,
+                                              group, 0, buf, buf_len);
+}
+
+int hbrbc_jit_decode_variant_file_name(size_t data_shards, size_t parity_shards,
+                                       const uint8_t *present, size_t rows_per_block,
+                                       size_t group, int fused_unframe, char *buf,
+                                       size_t buf_len) {
     std::vector<uint8_t> mat;
     const size_t n = data_shards + parity_shards;
     if (!present || !buf || data_shards == 0 || n > 256 || !build_matrix(data_shards, n, mat))
@@ -1844,7 +1907,8 @@ int hbrbc_jit_decode_file_name(size_t data_shards, size_t parity_shards, const u
     std::vector<XorProgram> progs;
     uint64_t hash;
     int rt;
-    if (!decode_programs(mat, data_shards, n, present, rb, progs, hash, rt) || group >= progs.size())
+    if (!decode_programs(mat, data_shards, n, present, rb, progs, hash, rt, fused_unframe != 0) ||
+        group >= progs.size())
         return fail(HBRBC_E_INVALID_ARG, "no such decoder group");
     const std::string f = jit_file("", progs[group].name).substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
@@ -1908,8 +1972,9 @@ int hbrbc_unframe_fused(const hbrbc_ctx *c, size_t shard_len, size_t payload_str
     if (rows_per_block && rows_per_block < c->n) rows.rb = (uint32_t)rows_per_block;
     const auto ds = c->dec_spec.find(code_rb(rows));
     const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
-    (void)spec;   // pattern decoders unframe too (v17 code objects)
-    return unframe_fusable(c, shard_len, payload_stride) ? 1 : 0;
+    // with a specialised decoder, its _uf variant (untried: assumed loadable)
+    return unframe_fusable(c, shard_len, payload_stride) && (!spec || ds->second.uf_state >= 0)
+               ? 1 : 0;
 }
 
 // ---- threshold-decrypt share verification (pairing.hip) ----

@@ -27,7 +27,7 @@
 // (tests compare both with the oracle).
 //
 // Code objects are cached as files under <lib dir>/jit (names from
-// encode_kernel_name / decode_kernel_name + "_v17.co");
+// encode_kernel_name / decode_kernel_name + "_v19.co");
 // __graft_entry__.build() pre-generates the encoders of the BASELINE
 // validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
@@ -96,9 +96,13 @@ __device__ __forceinline__ void hb_frame_head2(const u32x4 qa, unsigned P, unsig
     const uint32_t w[5] = {__builtin_bswap32(P), qa[0], qa[1], qa[2], qa[3]};
     _Pragma("unroll") for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], lb);
 }
-// Fused unframe: 16 bytes of data row `row` at byte `pos` are payload bytes
-// row*S + pos - 4 .. +15 (S % 4 == 0: dword-aligned; the 4-byte length prefix
-// and the row padding are not payload) -- kernels.hip unframe_put.
+// Fused unframe (the `_uf` decoder variants only): 16 bytes of data row `row`
+// at byte `pos` are payload bytes row*S + pos - 4 .. +15 (S % 4 == 0:
+// dword-aligned; the 4-byte length prefix and the row padding are not
+// payload) -- kernels.hip unframe_put.  Any payload code in a decoder slows
+// it even when unused (a branch splits the straight-line program; dropped
+// buffer stores still hold the load pipeline's vmcnt waits), so the plain
+// decoders carry none and a call that fuses loads the _uf programs.
 typedef unsigned int hb_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ void hb_uf_put(uint8_t *pb, unsigned S, unsigned row, unsigned pos,
                                           uint32_t a, uint32_t b, uint32_t c, uint32_t d) {

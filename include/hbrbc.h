@@ -356,6 +356,16 @@ int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t 
 size_t hbrbc_jit_decode_groups(size_t data_shards, size_t parity_shards, const uint8_t *present);
 int hbrbc_jit_build_decode(size_t data_shards, size_t parity_shards, const uint8_t *present,
                            size_t rows_per_block, size_t group, const char *dir);
+/* The same for the decoder's fused-unframe variant (fused_unframe != 0: the
+ * programs also write the payload bytes of the data rows; a decode that
+ * unframes in the reconstruct loads them on first use). */
+int hbrbc_jit_build_decode_variant(size_t data_shards, size_t parity_shards,
+                                   const uint8_t *present, size_t rows_per_block, size_t group,
+                                   int fused_unframe, const char *dir);
+int hbrbc_jit_decode_variant_file_name(size_t data_shards, size_t parity_shards,
+                                       const uint8_t *present, size_t rows_per_block,
+                                       size_t group, int fused_unframe, char *buf,
+                                       size_t buf_len);
 int hbrbc_jit_decode_file_name(size_t data_shards, size_t parity_shards, const uint8_t *present,
                                size_t rows_per_block, size_t group, char *buf, size_t buf_len);
 
