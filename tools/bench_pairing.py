@@ -2,8 +2,8 @@
 """Times hbrbc_pairing_check_batch (f4) on the GPU: `--n` checks e(a,b) ==
 e(c,d) in the verify_decryption_share shape, from a small pool of points
 built by the CPU restatement (dev tooling; bench.py's f4 leg generates its
-own inputs).  Prints one JSON line; HBRBC_PAIR_WAVES picks the kernel
-occupancy variant (read once per process)."""
+own inputs).  Prints one JSON line; HBRBC_PAIR_MULTI=0 selects one lane per
+pairing instead of the multi-Miller check kernel."""
 import argparse
 import json
 import os
@@ -58,7 +58,7 @@ def main():
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = sorted(times)[len(times) // 2]
-    print(json.dumps({"n_checks": a.n, "waves": os.environ.get("HBRBC_PAIR_WAVES", "default"),
+    print(json.dumps({"n_checks": a.n, "mode": "plain",
                       "ms": t * 1e3, "checks_per_s": a.n / t, "pairings_per_s": 2 * a.n / t,
                       "outcomes_exact": True}), flush=True)
 
