@@ -456,7 +456,7 @@ def max_over_ranks(x, world, dev):
 
 
 # ------------------------------------------------------------ validator mode --
-def run_validators(args, n, plen, count, rank, world, dev, local):
+def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     """Validator-sharded simulation: each rank proposes `count`
     instances per step and hosts N/world validators; Value rows cross ranks in
     an all-to-all, Echo rows in an all-gather (RCCL over xGMI), and every rank
@@ -504,6 +504,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
         s_.rb.profile_reset()
     timer.reset()
     timer.timing = world > 1
+    ex.reset_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -519,6 +520,18 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
     elapsed = max_over_ranks(elapsed, world, dev)
     xms = timer.elapsed_ms() / args.steps if world > 1 else 0.0
     timer.timing = False
+    # per-rank record of the exchange: world, backend, and per collective the
+    # calls and bytes this rank sent during the timed steps (rank 0 prints all)
+    mine = {"rank": rank, "world": world, "backend": ex.backend,
+            "device": str(dev), "exchange_ms_per_step": xms,
+            "collectives": {k_: {"calls_per_step": v_["calls"] / args.steps,
+                                 "bytes_sent_per_step": v_["bytes_sent"] / args.steps}
+                            for k_, v_ in sorted(ex.stats.items())}}
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    else:
+        per_rank = [mine]
     stages = {}
     counts = {}
     for s_ in subs:
@@ -541,14 +554,14 @@ def run_validators(args, n, plen, count, rank, world, dev, local):
         "config": {"workload": "%s validator-sharded: N=%d f=%d (%d+%d shards), %d B payloads, %d "
                                "proposals/GPU/step, validators in blocks of %d over %d GPUs, Value "
                                "all-to-all + Echo all-gather, every GPU decodes every instance"
-                               % (args.config, n, t.f, sb.rb.k, sb.rb.m, plen, count, t.rpg, world),
+                               % (config or args.config, n, t.f, sb.rb.k, sb.rb.m, plen, count, t.rpg,
+                                  world),
                    "proposals_per_gpu": count, "instances_per_step": count * world,
                    "parallelism": "validator-sharded x%d" % world,
                    "pipelined_sub_batches": nsub},
         "exchange": {"ms_per_step": xms, "bytes_per_step_per_gpu": xbytes,
                      "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
-                     "backend": getattr(ex, "dist", None) and ex.dist.get_backend()
-                     if world > 1 else "none"},
+                     "backend": ex.backend, "per_rank": per_rank},
         "work_per_step_rank0": counts,
         "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
     }
@@ -779,7 +792,8 @@ def main():
         torch.cuda.empty_cache()
         n4, plen4, _, _, vcount4 = CONFIGS["cfg4"]
         try:
-            v4 = run_validators(args, n4, plen4, args.vcount or vcount4, rank, world, dev, local)
+            v4 = run_validators(args, n4, plen4, args.vcount or vcount4, rank, world, dev, local,
+                                config="cfg4")
         except Exception as e:  # noqa: BLE001  (secondary object: keep the headline line)
             v4 = {"error": "%s: %s" % (type(e).__name__, e)}
             print("bench: cfg4 validator-sharded run failed: %r" % (e,), file=sys.stderr)
@@ -816,6 +830,9 @@ def main():
                 "config": head["config"], "roofline": head["roofline"], "cpu_baseline": cpu,
                 "stages_ms_per_step": head["stages_ms_per_step"],
             }
+            if cpu is None and world > 1:
+                line["cpu_baseline_note"] = ("measured on rank 0 of the N=1 run only (bench "
+                                             "contract); see that line's cpu_baseline")
             if vobj is not None:
                 if cpu is not None and "error" not in vobj:
                     vobj["cpu_baseline"] = dict(cpu, note="the same per-instance pipeline; the "

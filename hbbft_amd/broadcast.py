@@ -297,6 +297,12 @@ class Broadcast:
         """broadcast.rs:142-153."""
         if not self.val_set.contains(sender_id):
             raise BroadcastError(ErrorKind.UnknownSender)
+        if self._decode_pending is not None:
+            # a deferred decode decides this instance's next state: the caller
+            # must resolve it first (decode_sink is run_lockstep's contract:
+            # one message per instance per round, then resolve_decodes)
+            raise RuntimeError("%r: message delivered while a deferred decode is pending; "
+                               "call resolve_decodes() first" % (self,))
         k = message.kind
         if k == Message.VALUE:
             return self._handle_value(sender_id, message.payload)
@@ -476,6 +482,9 @@ class Broadcast:
         if self._decode_pending is not None:
             # a second attempt within the same message: same inputs, same outcome
             # (nothing on success, another decoding fault on failure)
+            if self._decode_pending["root"] != h:
+                raise RuntimeError("%r: second decode for another root while one is pending"
+                                   % (self,))
             self._decode_pending["repeat"] += 1
             return Step()
         leaf_values = []

@@ -531,6 +531,8 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
         c->pc_inserted = 0;
     }
     c->pc_inserted += count;
+    const auto ds = c->dec_spec.find(code_rb(rows));
+    const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
     {
         StageTimer t(c, HBRBC_STAGE_DECODE_MATRIX, s);
         DecodeMatrixArgs a;
@@ -544,12 +546,14 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
         a.pat = c->ws_pat.as<int>();
         a.own = c->ws_own.as<uint8_t>();
         a.status = status;
+        if (spec) {   // slots of the specialised pattern's hash hold only that pattern
+            a.spec_hash = ds->second.hash;
+            pattern_mask(ds->second.present.data(), (int)c->n, a.spec_mask);
+        }
         HB_HIP(launch_decode_matrix(a, s));
     }
     if (c->m == 0) return HBRBC_OK;  // Coding::Trivial: nothing to rebuild
     StageTimer t(c, HBRBC_STAGE_RECONSTRUCT, s);
-    const auto ds = c->dec_spec.find(code_rb(rows));
-    const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
     // fusing with a specialised decoder needs its _uf variant
     if (spec && uf_payload && !uf_decoder(c, ds->second, code_rb(rows))) uf_payload = nullptr;
     if (spec) {

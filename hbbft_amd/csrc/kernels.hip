@@ -391,7 +391,7 @@ __global__ HB_SPONGE_ATTR void leaf_hash_kernel(
     if (g >= total) return;
     const size_t inst = g / n;
     const uint32_t i = (uint32_t)(g - inst * n);
-    if (slens) S = slens[inst];
+    if (slens) S = min(slens[inst], (uint32_t)rows.sst);   // never past the row slot
     uint32_t d[8];
     sha3_256_row<V16>(shards + inst * inst_stride + rows.off(i), S, d);
     store_digest(nodes + inst * node_inst_stride + (size_t)i * 32, d);
@@ -415,7 +415,8 @@ __global__ HB_SPONGE_ATTR void merkle_tree_kernel(
     uint8_t *ns = nodes + inst * node_inst_stride;
     if (active) {
         uint32_t d[8];
-        sha3_256_row<V16>(shards + inst * inst_stride + rows.off(leaf), slens ? slens[inst] : S, d);
+        sha3_256_row<V16>(shards + inst * inst_stride + rows.off(leaf),
+                          slens ? min(slens[inst], (uint32_t)rows.sst) : S, d);
         store_digest(ns + (size_t)leaf * 32, d);
         lvl[0][threadIdx.x][0] = make_uint4(d[0], d[1], d[2], d[3]);
         lvl[0][threadIdx.x][1] = make_uint4(d[4], d[5], d[6], d[7]);
@@ -661,9 +662,18 @@ __host__ __device__ __forceinline__ uint64_t pat_hash_words(const uint32_t (&w)[
 // 64-bit hash) joins the slot; an empty slot is claimed by CAS (this
 // instance then computes it); a table at half load or 32 probes without
 // success send the instance to its private slot cap + inst.
+//
+// spec_hash != 0: the hash of the pattern a specialised decoder serves.  The
+// decoders (jit.hip guard) and the generic kernel's skip test route by slot
+// hash alone, so an instance whose mask collides with that hash but differs
+// from spec_mask never enters the table (private slot, generic kernel).
+struct SpecKey {
+    uint64_t hash;
+    uint32_t mask[8];
+};
 __global__ __launch_bounds__(kBlock) void pattern_lookup_kernel(
     int n, const uint8_t *__restrict__ present, size_t count, PatternCache c,
-    int *__restrict__ pat, uint8_t *__restrict__ own) {
+    int *__restrict__ pat, uint8_t *__restrict__ own, SpecKey spec) {
     const size_t inst = blockIdx.x * (size_t)kBlock + threadIdx.x;
     if (inst >= count) return;
     const uint8_t *pres = present + inst * (size_t)n;
@@ -671,9 +681,14 @@ __global__ __launch_bounds__(kBlock) void pattern_lookup_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = mask_word(pres, n, i);
     const uint64_t h = pat_hash_words(w, n);
+    bool spec_collision = false;
+    if (spec.hash && h == spec.hash) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) spec_collision |= w[i] != spec.mask[i];
+    }
     const bool may_insert = *reinterpret_cast<volatile uint32_t *>(c.fill) < (uint32_t)(c.cap / 2);
     int slot = (int)(h & (uint64_t)(c.cap - 1)), found = -1, mine = 0;
-    for (int probe = 0; probe < 32; ++probe) {
+    for (int probe = spec_collision ? 32 : 0; probe < 32; ++probe) {
         unsigned long long cur = reinterpret_cast<volatile unsigned long long *>(c.hash)[slot];
         if (cur == 0 && may_insert) {
             cur = atomicCAS(reinterpret_cast<unsigned long long *>(c.hash) + slot, 0ull,
@@ -990,10 +1005,15 @@ constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kern
 bool few_sponges(size_t lanes) { return lanes < ((size_t)1 << 18); }
 }  // namespace
 
-uint64_t pattern_hash(const uint8_t *present, int n) {
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+void pattern_mask(const uint8_t *present, int n, uint32_t (&w)[8]) {
+    for (int i = 0; i < 8; ++i) w[i] = 0;
     for (int i = 0; i < n && i < 256; ++i)
         if (present[i]) w[i / 32] |= 1u << (i % 32);
+}
+
+uint64_t pattern_hash(const uint8_t *present, int n) {
+    uint32_t w[8];
+    pattern_mask(present, n, w);
     return pat_hash_words(w, n);
 }
 
@@ -1212,8 +1232,11 @@ hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
 
 hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
+    SpecKey spec;
+    spec.hash = a.spec_hash;
+    for (int i = 0; i < 8; ++i) spec.mask[i] = a.spec_mask[i];
     hipLaunchKernelGGL(pattern_lookup_kernel, dim3(grid_for(a.count, (size_t)1 << 30)),
-                       dim3(kBlock), 0, s, a.n, a.present, a.count, a.cache, a.pat, a.own);
+                       dim3(kBlock), 0, s, a.n, a.present, a.count, a.cache, a.pat, a.own, spec);
     const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
     // threads per instance by system size (measured per step): k = 22 one
     // wave, 0.46 -> 0.34 ms (no cross-wave barriers, more instances per CU);

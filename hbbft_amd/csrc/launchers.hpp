@@ -164,12 +164,20 @@ struct DecodeMatrixArgs {
     int *pat;                   // [count] -> slot
     uint8_t *own;               // [count]: this instance computes its slot
     int32_t *status;            // [count] out
+    // the pattern a specialised decoder serves (spec_hash 0: none).  Its
+    // decoders and the generic kernel route instances by slot hash alone, so
+    // a slot with that hash may only ever hold that pattern: an instance whose
+    // mask hashes to spec_hash but differs goes to its private slot
+    uint64_t spec_hash = 0;
+    uint32_t spec_mask[8] = {};
 };
 // lookup (slot per instance) -> decode matrix of new slots -> per-instance status
 hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s);
 // 64-bit hash of a present mask (as the lookup kernel computes it): lets the
 // host name the slot of a pattern it specialised a decoder for.
 uint64_t pattern_hash(const uint8_t *present, int n);
+// the 8 mask words of a present pattern (bit i of word i / 32 = present[i])
+void pattern_mask(const uint8_t *present, int n, uint32_t (&w)[8]);
 
 // Root compare + BE32 length parse (decode_from_shards tail).
 hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes,

@@ -21,8 +21,8 @@
 // ([144 words][pairings]), so every store and load is one coalesced dword per
 // lane.  Points arrive in the crate's uncompressed encodings (G1 96 bytes
 // x || y, G2 192 bytes x.c1 || x.c0 || y.c1 || y.c0, big-endian, flag bits
-// in byte 0) and are checked for canonical coordinates and curve membership;
-// subgroup membership is the caller's (the crate's deserialisation enforces it).
+// in byte 0) and are checked for canonical coordinates, curve membership and
+// membership of the order-r subgroup, as the crate's deserialisation does.
 //
 // Tower: Fp2 = Fp[u]/(u^2+1), Fp6 = Fp2[v]/(v^3 - (u+1)), Fp12 = Fp6[w]/(w^2 - v),
 // the crate's.  Miller loop over |x| = 0xd201000000010000 with homogeneous
@@ -645,6 +645,146 @@ DEV bool all_zero(const uint8_t *p, int n, uint8_t first_mask) {
 // Status of a decoded point: 0 ok, 1 infinity, 2 invalid.
 enum { PT_OK = 0, PT_INF = 1, PT_BAD = 2 };
 
+// ------------------------------------------------------- subgroup checks
+// The crate's deserialisation (`into_affine`: on-curve, then
+// is_in_correct_subgroup_assuming_on_curve = [r] P == O) rejects points of
+// E(Fp) / E'(Fp2) outside the order-r subgroup before any pairing.  Here the
+// equivalent endomorphism tests (Scott, ePrint 2021/1130 sec. 6, proof in
+// 2022/352): P in G1 iff phi(P) = (beta x, y) = -[x^2] P, and Q in G2 iff
+// psi(Q) = [x] Q, i.e. a 128-bit and a 64-bit scalar multiplication instead
+// of a 255-bit one.  oracle/bls_oracle.py restates the crate's [r] P test and
+// tests/test_pairing.py feeds on-curve points outside the subgroup (status 2).
+// Complete projective formulas for y^2 = x^3 + b (Renes-Costello-Batina 2016,
+// algorithms 7 and 9 with a = 0), so no exceptional case arises mid-chain.
+template <class F> struct PtProj { F x, y, z; };
+
+DEV void fe_mul(Fp &r, const Fp &a, const Fp &b) { fp_mul(r, a, b); }
+DEV void fe_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp2_mul_in(r, a, b); }
+DEV void fe_add(Fp &r, const Fp &a, const Fp &b) { fp_add(r, a, b); }
+DEV void fe_add(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp2_add(r, a, b); }
+DEV void fe_sub(Fp &r, const Fp &a, const Fp &b) { fp_sub(r, a, b); }
+DEV void fe_sub(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp2_sub(r, a, b); }
+DEV void fe_one(Fp &r) { fp_set(r, kOne); }
+DEV void fe_one(Fp2 &r) { fp_set(r.c0, kOne); fp_zero(r.c1); }
+// 3b: 12 on E, 12 (u + 1) on the twist
+DEV void fe_mul_b3(Fp &r, const Fp &a) {
+    Fp t;
+    fp_add(t, a, a);
+    fp_add(t, t, a);
+    fp_add(t, t, t);
+    fp_add(r, t, t);
+}
+DEV void fe_mul_b3(Fp2 &r, const Fp2 &a) {
+    Fp2 x;
+    fp2_mul_xi(x, a);
+    fe_mul_b3(r.c0, x.c0);
+    fe_mul_b3(r.c1, x.c1);
+}
+
+template <class F>
+NOINL void pt_dbl(PtProj<F> &p) {
+    F t0, t1, t2, x3, y3, z3;
+    fe_mul(t0, p.y, p.y);
+    fe_add(z3, t0, t0);
+    fe_add(z3, z3, z3);
+    fe_add(z3, z3, z3);
+    fe_mul(t1, p.y, p.z);
+    fe_mul(t2, p.z, p.z);
+    fe_mul_b3(t2, t2);
+    fe_mul(x3, t2, z3);
+    fe_add(y3, t0, t2);
+    fe_mul(z3, t1, z3);
+    fe_add(t1, t2, t2);
+    fe_add(t2, t1, t2);
+    fe_sub(t0, t0, t2);
+    fe_mul(y3, t0, y3);
+    fe_add(y3, x3, y3);
+    fe_mul(t1, p.x, p.y);
+    fe_mul(x3, t0, t1);
+    fe_add(p.x, x3, x3);
+    p.y = y3;
+    p.z = z3;
+}
+
+// p <- p + (qx, qy, 1)
+template <class F>
+NOINL void pt_add_affine(PtProj<F> &p, const F &qx, const F &qy) {
+    F t0, t1, t2, t3, t4, x3, y3, z3;
+    fe_mul(t0, p.x, qx);
+    fe_mul(t1, p.y, qy);
+    t2 = p.z;
+    fe_add(t3, p.x, p.y);
+    fe_add(t4, qx, qy);
+    fe_mul(t3, t3, t4);
+    fe_add(t4, t0, t1);
+    fe_sub(t3, t3, t4);
+    fe_mul(t4, qy, p.z);
+    fe_add(t4, t4, p.y);            // Y1 + Y2 Z1
+    fe_mul(y3, qx, p.z);
+    fe_add(y3, y3, p.x);            // X1 + X2 Z1
+    fe_add(x3, t0, t0);
+    fe_add(t0, x3, t0);
+    fe_mul_b3(t2, t2);
+    fe_add(z3, t1, t2);
+    fe_sub(t1, t1, t2);
+    fe_mul_b3(y3, y3);
+    fe_mul(x3, t4, y3);
+    fe_mul(t2, t3, t1);
+    fe_sub(x3, t2, x3);
+    fe_mul(y3, y3, t0);
+    fe_mul(t1, t1, z3);
+    fe_add(y3, t1, y3);
+    fe_mul(t0, t0, t3);
+    fe_mul(z3, z3, t4);
+    fe_add(p.z, z3, t0);
+    p.x = x3;
+    p.y = y3;
+}
+
+// [k] (x, y) for the bits of k below its leading one (k's top bit at `top`)
+template <class F>
+DEV void pt_mul_bits(PtProj<F> &acc, const F &x, const F &y, uint64_t hi, uint64_t lo, int top) {
+    acc.x = x;
+    acc.y = y;
+    fe_one(acc.z);
+    for (int b = top - 1; b >= 0; --b) {
+        pt_dbl(acc);
+        const uint64_t w = b >= 64 ? hi : lo;
+        if ((w >> (b & 63)) & 1u) pt_add_affine(acc, x, y);
+    }
+}
+
+// (x, y) affine (Montgomery form), already on E: phi(P) == -[x^2] P, i.e.
+// [x^2] P == (beta x, -y) in projective coordinates (Z != 0)
+NOINL bool g1_in_subgroup(const Fp &x, const Fp &y) {
+    PtProj<Fp> a;
+    pt_mul_bits(a, x, y, kXSqHi, kXSqLo, 127);
+    Fp bx, ny, l, r;
+    fp_set(bx, kBeta);
+    fp_mul(bx, bx, x);
+    fp_neg(ny, y);
+    fp_mul(l, bx, a.z);
+    fp_mul(r, ny, a.z);
+    return !fp_is_zero(a.z) && fp_eq(l, a.x) && fp_eq(r, a.y);
+}
+
+// (x, y) on E': psi(Q) == [x] Q = -[|x|] Q, i.e. [|x|] Q == (psi_x, -psi_y)
+NOINL bool g2_in_subgroup(const Fp2 &x, const Fp2 &y) {
+    PtProj<Fp2> a;
+    pt_mul_bits(a, x, y, 0, kXAbs, 63);
+    Fp2 cx, cy, px, py, l, r;
+    fp2_const(cx, kPsi[0]);
+    fp2_const(cy, kPsi[1]);
+    fp2_conj(px, x);
+    fp2_mul(px, px, cx);
+    fp2_conj(py, y);
+    fp2_mul(py, py, cy);
+    fp2_neg(py, py);
+    fp2_mul(l, px, a.z);
+    fp2_mul(r, py, a.z);
+    return !fp2_is_zero(a.z) && fp2_eq(l, a.x) && fp2_eq(r, a.y);
+}
+
 DEV int decode_g1(const uint8_t *src, Fp &x, Fp &y) {
     const uint8_t f = src[0];
     if (f & 0xA0) return PT_BAD;                       // compressed / sort flags
@@ -659,7 +799,8 @@ DEV int decode_g1(const uint8_t *src, Fp &x, Fp &y) {
     fp_mul(r, r, x);
     fp_set(b, kB1);
     fp_add(r, r, b);
-    return fp_eq(l, r) ? PT_OK : PT_BAD;               // y^2 = x^3 + 4
+    if (!fp_eq(l, r)) return PT_BAD;                   // y^2 = x^3 + 4
+    return g1_in_subgroup(x, y) ? PT_OK : PT_BAD;      // order r (the crate's into_affine)
 }
 
 DEV int decode_g2(const uint8_t *src, Fp2 &x, Fp2 &y) {
@@ -681,7 +822,8 @@ DEV int decode_g2(const uint8_t *src, Fp2 &x, Fp2 &y) {
     fp_set(bb.c0, kB1);
     bb.c1 = bb.c0;                                     // 4 (u + 1)
     fp2_add(r, r, bb);
-    return fp2_eq(l, r) ? PT_OK : PT_BAD;
+    if (!fp2_eq(l, r)) return PT_BAD;
+    return g2_in_subgroup(x, y) ? PT_OK : PT_BAD;
 }
 
 // Limb-major workspace: word w of pairing i at ws[w * n + i].

@@ -93,11 +93,32 @@ class Topology:
 
 
 # ---------------------------------------------------------------- exchange ---
+class _StagedWork:
+    """Handle of a host-staged (gloo) collective issued with async_op: wait()
+    waits for the gloo work, then copies the host result into the device
+    tensor on the current stream -- the same point at which an NCCL handle's
+    wait() makes the current stream wait for the RCCL kernel, so the staged
+    rehearsal runs the handle/event ordering of the RCCL path."""
+
+    def __init__(self, work, host_out, out):
+        self.work, self.host_out, self.out = work, host_out, out
+
+    def wait(self):
+        self.work.wait()
+        if self.out is not None:
+            self.out.copy_(self.host_out())
+        self.work = self.out = None
+
+
 class DistExchange:
     """all-to-all / all-gather over a torch.distributed group.  With NCCL
     (= RCCL on ROCm) the device buffers go straight over xGMI; with gloo
     (CPU tests, several ranks sharing one GPU) device tensors are staged
-    through host memory."""
+    through host memory.  Both backends return a handle when async_op is set
+    (wait() = the current stream / host waits for the exchange, and for gloo
+    the copy back to the device), so the pipelined schedule is the same code
+    on both.  Every call is counted per collective name: calls and bytes this
+    rank sends (bench line, `exchange.per_rank`)."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -105,38 +126,59 @@ class DistExchange:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.staged = dist.get_backend(group) != "nccl"
+        self.backend = dist.get_backend(group)
+        self.staged = self.backend != "nccl"
+        self.stats = {}
 
-    def all_to_all(self, out, inp, async_op=False):
+    def _count(self, name, nbytes):
+        e = self.stats.setdefault(name, {"calls": 0, "bytes_sent": 0})
+        e["calls"] += 1
+        e["bytes_sent"] += int(nbytes)
+
+    def reset_stats(self):
+        self.stats = {}
+
+    def all_to_all(self, out, inp, async_op=False, name="all_to_all"):
         """out[s] on this rank = inp[rank] on rank s (dim 0 = ranks).  With
-        async_op (NCCL only) returns a handle; wait() makes the current stream
-        wait for it."""
+        async_op returns a handle whose wait() makes the current stream wait."""
         assert out.shape[0] == self.world and inp.shape[0] == self.world
+        assert out.is_contiguous() and inp.is_contiguous()
         if self.world == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             return None
+        # this rank keeps chunk `rank` and sends the other world - 1
+        self._count(name, inp.numel() * inp.element_size() * (self.world - 1) // self.world)
         if self.staged and out.is_cuda:
-            o, i = out.cpu(), inp.cpu()
-            self.dist.all_to_all_single(o, i, group=self.group)
+            o, i = torch.empty(out.shape, dtype=out.dtype), inp.cpu()
+            w = self.dist.all_to_all_single(o, i, group=self.group, async_op=async_op)
+            if async_op:
+                return _StagedWork(w, lambda: o, out)
             out.copy_(o)
             return None
-        return self.dist.all_to_all_single(out, inp, group=self.group,
-                                           async_op=async_op and not self.staged)
+        return self.dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
 
-    def all_gather(self, out, inp, async_op=False):
+    def all_gather(self, out, inp, async_op=False, name="all_gather"):
         """out[s] = inp of rank s (dim 0 of out = ranks, inp flat or not)."""
         assert out.shape[0] == self.world and out.numel() == self.world * inp.numel()
+        assert out.is_contiguous() and inp.is_contiguous()
         if self.world == 1:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.reshape(-1))
             return None
-        if self.staged:
-            parts = [torch.empty_like(inp, device="cpu") for _ in range(self.world)]
-            self.dist.all_gather(parts, inp.cpu(), group=self.group)
-            out.view(self.world, -1).copy_(torch.stack([p.reshape(-1) for p in parts]))
+        # every other rank receives this rank's chunk
+        self._count(name, inp.numel() * inp.element_size() * (self.world - 1))
+        if self.staged and out.is_cuda:
+            parts = [torch.empty(inp.shape, dtype=inp.dtype) for _ in range(self.world)]
+            w = self.dist.all_gather(parts, inp.cpu(), group=self.group, async_op=async_op)
+
+            def host():
+                return torch.stack([p.reshape(-1) for p in parts]).view(out.shape)
+            if async_op:
+                return _StagedWork(w, host, out)
+            out.copy_(host())
             return None
-        return self.dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=self.group,
+        return self.dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group,
                                                 async_op=async_op)
 
 
@@ -144,15 +186,19 @@ class SoloExchange:
     """The exchange of a one-rank run (no process group): ShardedBroadcast
     aliases its buffers, so nothing moves."""
 
-    world, rank, staged = 1, 0, True
+    world, rank, staged, backend = 1, 0, True, "none"
+    stats = {}
 
-    def all_to_all(self, out, inp, async_op=False):
+    def all_to_all(self, out, inp, async_op=False, name=None):
         if out.data_ptr() != inp.data_ptr():
             out.copy_(inp)
 
-    def all_gather(self, out, inp, async_op=False):
+    def all_gather(self, out, inp, async_op=False, name=None):
         if out.data_ptr() != inp.data_ptr():
             out.view(-1).copy_(inp.reshape(-1))
+
+    def reset_stats(self):
+        pass
 
 
 class CommTimer:
@@ -304,9 +350,9 @@ class ShardedBroadcast:
         if self.world == 1:
             self.roots_all[0].copy_(self._roots)
             return []
-        return [ex.all_to_all(self.recv_sh, self.slab, async_op),
-                ex.all_to_all(self.recv_dg, self.send_dg, async_op),
-                ex.all_gather(self.roots_all, self._roots, async_op)]
+        return [ex.all_to_all(self.recv_sh, self.slab, async_op, name="value_shards"),
+                ex.all_to_all(self.recv_dg, self.send_dg, async_op, name="value_proofs"),
+                ex.all_gather(self.roots_all, self._roots, async_op, name="roots")]
 
     # 3. validators validate their Values --------------------------------------
     def validate_values(self):
@@ -330,9 +376,9 @@ class ShardedBroadcast:
     def exchange_echo(self, ex, async_op=False):
         if self.world == 1:
             return []
-        return [ex.all_gather(self.echo_sh, self.recv_sh, async_op),
-                ex.all_gather(self.echo_dg, self.recv_dg, async_op),
-                ex.all_gather(self.okv_all, self.ok_pad, async_op)]
+        return [ex.all_gather(self.echo_sh, self.recv_sh, async_op, name="echo_shards"),
+                ex.all_gather(self.echo_dg, self.recv_dg, async_op, name="echo_proofs"),
+                ex.all_gather(self.okv_all, self.ok_pad, async_op, name="echo_value_ok")]
 
     def validate_echoes(self):
         """Proof::validate of every Echo the receiver gets from other ranks'

@@ -168,7 +168,9 @@ int hbrbc_frame_encode_ragged(hbrbc_ctx *ctx, const uint8_t *payloads, size_t pa
                               uint8_t *shards, size_t shard_stride, size_t inst_stride,
                               void *stream);
 /* MerkleTree::from_vec of a ragged batch: leaf j of instance i hashes
- * shard_lens[i] (device uint32[count]) bytes of its row. */
+ * shard_lens[i] (device uint32[count]) bytes of its row.  Each entry must be
+ * <= shard_stride; the kernels clamp a larger one to shard_stride (they never
+ * read past the row slot), so its digests then cover shard_stride bytes. */
 int hbrbc_merkle_ragged(hbrbc_ctx *ctx, const uint8_t *shards, const uint32_t *shard_lens,
                         size_t shard_stride, size_t inst_stride, size_t count, uint8_t *nodes,
                         size_t node_inst_stride, void *stream);

@@ -168,6 +168,85 @@ def g1_neg(pt):
     return None if pt is None else (pt[0], (-pt[1]) % P)
 
 
+# ---------------------------------------------------------------- subgroup membership
+# The crate's deserialisation (`EncodedPoint::into_affine`) checks the curve
+# equation and then `is_in_correct_subgroup_assuming_on_curve`: [r] P == O
+# (the order-r subgroup; E(Fp) has cofactor h1, E'(Fp2) cofactor h2).  The HIP
+# decoders use the equivalent endomorphism tests (pairing.hip); the tests
+# compare both on points inside and outside the subgroup.
+def g1_in_subgroup(pt):
+    return pt is None or (g1_on_curve(pt) and _smul(g1_add, pt, R) is None)
+
+
+def g2_in_subgroup(pt):
+    return pt is None or (g2_on_curve(pt) and _smul(g2_add, pt, R) is None)
+
+
+BETA = 0x5f19672fdf76ce51ba69c6076a0f77eaddb3a93be6f89688de17d813620a00022e01fffffffefffe
+
+
+def g1_endo_test(pt):
+    """Scott's G1 test: phi(P) = (beta x, y) == -[x^2] P."""
+    return (BETA * pt[0] % P, pt[1]) == g1_neg(_smul(g1_add, pt, X_ABS * X_ABS))
+
+
+def _f2pow(a, e):
+    out = F2_ONE
+    while e:
+        if e & 1:
+            out = f2mul(out, a)
+        a = f2mul(a, a)
+        e >>= 1
+    return out
+
+
+def psi(q):
+    """Untwist-Frobenius-twist on E': (conj(x) xi^-((p-1)/3), conj(y) xi^-((p-1)/2))."""
+    cx, cy = f2inv(_f2pow(XI, (P - 1) // 3)), f2inv(_f2pow(XI, (P - 1) // 2))
+    x, y = q
+    return (f2mul((x[0], (-x[1]) % P), cx), f2mul((y[0], (-y[1]) % P), cy))
+
+
+def g2_endo_test(q):
+    """Scott's G2 test: psi(Q) == [x] Q = -[|x|] Q."""
+    t = _smul(g2_add, q, X_ABS)
+    return t is not None and psi(q) == (t[0], f2neg(t[1]))
+
+
+def _f2sqrt(a):
+    """Square root in Fp2 (p = 3 mod 4), or None."""
+    a1 = _f2pow(a, (P - 3) // 4)
+    alpha = f2mul(f2mul(a1, a1), a)
+    x0 = f2mul(a1, a)
+    if f2eq(alpha, (P - 1, 0)):
+        x = f2mul((0, 1), x0)
+    else:
+        x = f2mul(_f2pow(f2add(F2_ONE, alpha), (P - 1) // 2), x0)
+    return x if f2eq(f2mul(x, x), a) else None
+
+
+def g1_curve_point(seed):
+    """A point of E(Fp) from a seed (the first x >= seed on the curve), almost
+    surely outside G1 (the probability of landing in it is 1/h1)."""
+    x = seed % P
+    while True:
+        a = (x * x * x + B1) % P
+        y = pow(a, (P + 1) // 4, P)
+        if y * y % P == a:
+            return (x, y)
+        x += 1
+
+
+def g2_curve_point(seed):
+    """A point of E'(Fp2) from a seed, almost surely outside G2."""
+    x = (seed % P, 1)
+    while True:
+        y = _f2sqrt(f2add(f2mul(f2mul(x, x), x), B2))
+        if y is not None:
+            return (x, y)
+        x = (x[0] + 1, 1)
+
+
 # ---------------------------------------------------------------- Fp12 = Fp[w]/(w^12 - 2w^6 + 2)
 def f12(coeffs):
     return [c % P for c in coeffs]

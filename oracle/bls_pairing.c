@@ -569,7 +569,80 @@ static int zero_rest(const uint8_t *s, int n) {
         if (s[i]) return 0;
     return 1;
 }
-/* 0 ok, 1 infinity, 2 invalid */
+/* Subgroup membership as the crate's deserialisation checks it
+ * (`into_affine` -> is_in_correct_subgroup_assuming_on_curve): [r] P == O,
+ * by double-and-add over r with the complete projective formulas for
+ * y^2 = x^3 + b (Renes-Costello-Batina 2016, algorithms 7 and 9, a = 0). */
+static const uint64_t RORD[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull,
+                                 0x3339d80809a1d805ull, 0x73eda753299d7d48ull};
+typedef struct { fp x, y, z; } p1p;
+typedef struct { fp2 x, y, z; } p2p;
+static void b3_1(fp *r, const fp *a) {   /* 3b = 12 */
+    fp t;
+    fp_add(&t, a, a);
+    fp_add(&t, &t, a);
+    fp_add(&t, &t, &t);
+    fp_add(r, &t, &t);
+}
+static void b3_2(fp2 *r, const fp2 *a) {  /* 3b = 12 (u + 1) */
+    fp2 t;
+    f2_mul_xi(&t, a);
+    b3_1(&r->c0, &t.c0);
+    b3_1(&r->c1, &t.c1);
+}
+#define PT_DBL(NAME, T, PT, MUL, ADD, SUB, B3)                                        \
+    static void NAME(PT *p) {                                                         \
+        T t0, t1, t2, x3, y3, z3;                                                     \
+        MUL(&t0, &p->y, &p->y); ADD(&z3, &t0, &t0); ADD(&z3, &z3, &z3);               \
+        ADD(&z3, &z3, &z3); MUL(&t1, &p->y, &p->z); MUL(&t2, &p->z, &p->z);           \
+        B3(&t2, &t2); MUL(&x3, &t2, &z3); ADD(&y3, &t0, &t2); MUL(&z3, &t1, &z3);     \
+        ADD(&t1, &t2, &t2); ADD(&t2, &t1, &t2); SUB(&t0, &t0, &t2);                   \
+        MUL(&y3, &t0, &y3); ADD(&y3, &x3, &y3); MUL(&t1, &p->x, &p->y);              \
+        MUL(&x3, &t0, &t1); ADD(&p->x, &x3, &x3); p->y = y3; p->z = z3;              \
+    }
+#define PT_ADD(NAME, T, PT, MUL, ADD, SUB, B3)                                        \
+    static void NAME(PT *p, const PT *q) {                                            \
+        T t0, t1, t2, t3, t4, x3, y3, z3;                                             \
+        MUL(&t0, &p->x, &q->x); MUL(&t1, &p->y, &q->y); MUL(&t2, &p->z, &q->z);       \
+        ADD(&t3, &p->x, &p->y); ADD(&t4, &q->x, &q->y); MUL(&t3, &t3, &t4);           \
+        ADD(&t4, &t0, &t1); SUB(&t3, &t3, &t4); ADD(&t4, &p->y, &p->z);               \
+        ADD(&x3, &q->y, &q->z); MUL(&t4, &t4, &x3); ADD(&x3, &t1, &t2);               \
+        SUB(&t4, &t4, &x3); ADD(&x3, &p->x, &p->z); ADD(&y3, &q->x, &q->z);           \
+        MUL(&x3, &x3, &y3); ADD(&y3, &t0, &t2); SUB(&y3, &x3, &y3);                   \
+        ADD(&x3, &t0, &t0); ADD(&t0, &x3, &t0); B3(&t2, &t2); ADD(&z3, &t1, &t2);     \
+        SUB(&t1, &t1, &t2); B3(&y3, &y3); MUL(&x3, &t4, &y3); MUL(&t2, &t3, &t1);     \
+        SUB(&x3, &t2, &x3); MUL(&y3, &y3, &t0); MUL(&t1, &t1, &z3);                   \
+        ADD(&y3, &t1, &y3); MUL(&t0, &t0, &t3); MUL(&z3, &z3, &t4);                   \
+        ADD(&p->z, &z3, &t0); p->x = x3; p->y = y3;                                   \
+    }
+PT_DBL(p1_dbl, fp, p1p, fp_mul, fp_add, fp_sub, b3_1)
+PT_ADD(p1_add, fp, p1p, fp_mul, fp_add, fp_sub, b3_1)
+PT_DBL(p2_dbl, fp2, p2p, f2_mul, f2_add, f2_sub, b3_2)
+PT_ADD(p2_add, fp2, p2p, f2_mul, f2_add, f2_sub, b3_2)
+static int fp_zero_p(const fp *a) {
+    for (int i = 0; i < 6; ++i)
+        if (a->l[i]) return 0;
+    return 1;
+}
+static int g1_r_torsion(const fp *x, const fp *y) {
+    p1p q = {*x, *y, ONE}, acc = q;
+    for (int b = 253; b >= 0; --b) {   /* r < 2^255, top bit 254 */
+        p1_dbl(&acc);
+        if ((RORD[b >> 6] >> (b & 63)) & 1) p1_add(&acc, &q);
+    }
+    return fp_zero_p(&acc.z);
+}
+static int g2_r_torsion(const fp2 *x, const fp2 *y) {
+    fp2 one = {ONE, {{0}}};
+    p2p q = {*x, *y, one}, acc = q;
+    for (int b = 253; b >= 0; --b) {
+        p2_dbl(&acc);
+        if ((RORD[b >> 6] >> (b & 63)) & 1) p2_add(&acc, &q);
+    }
+    return fp_zero_p(&acc.z.c0) && fp_zero_p(&acc.z.c1);
+}
+
+/* 0 ok, 1 infinity, 2 invalid (encoding, curve equation, or subgroup) */
 static int dec_g1(const uint8_t *s, fp *x, fp *y) {
     if (s[0] & 0xA0) return 2;
     if (s[0] & 0x40) return zero_rest(s, 96) ? 1 : 2;
@@ -579,7 +652,8 @@ static int dec_g1(const uint8_t *s, fp *x, fp *y) {
     fp_mul(&r, x, x);
     fp_mul(&r, &r, x);
     fp_add(&r, &r, &B1);
-    return fp_eq(&l, &r) ? 0 : 2;
+    if (!fp_eq(&l, &r)) return 2;
+    return g1_r_torsion(x, y) ? 0 : 2;
 }
 static int dec_g2(const uint8_t *s, fp2 *x, fp2 *y) {
     if (s[0] & 0xA0) return 2;
@@ -592,7 +666,8 @@ static int dec_g2(const uint8_t *s, fp2 *x, fp2 *y) {
     f2_sqr(&r, x);
     f2_mul(&r, &r, x);
     f2_add(&r, &r, &b);
-    return (fp_eq(&l.c0, &r.c0) && fp_eq(&l.c1, &r.c1)) ? 0 : 2;
+    if (!(fp_eq(&l.c0, &r.c0) && fp_eq(&l.c1, &r.c1))) return 2;
+    return g2_r_torsion(x, y) ? 0 : 2;
 }
 
 /* e(g1, g2) -> 576 GT bytes (tower order, big-endian); returns 0 ok, 2 invalid */

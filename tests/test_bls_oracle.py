@@ -86,3 +86,45 @@ def test_c_restatement_matches_golden_and_python():
     assert bls_c.check(bytes([g1[0] | 0x80]) + g1[1:], g2, g1, g2) == 2
     gt, st = bls_c.pairing(B.g1_bytes(None), g2)
     assert st == 0 and gt == B.gt_bytes(B.F12_ONE)
+
+
+def test_endomorphism_subgroup_tests_match_r_torsion():
+    """The HIP decoders test subgroup membership with Scott's endomorphism
+    checks (phi(P) == -[x^2] P on G1, psi(Q) == [x] Q on G2); the crate checks
+    [r] P == O.  Both agree on subgroup points and on on-curve points outside
+    the subgroup (plain curve points, and subgroup points plus a point of
+    cofactor order); beta is the cube root the generator selects."""
+    rng = random.Random(5)
+    assert B.g1_endo_test(B.G1_GEN) and B.g2_endo_test(B.G2_GEN)
+    other_beta = B.BETA * B.BETA % B.P
+    assert (other_beta * B.G1_GEN[0] % B.P, B.G1_GEN[1]) != B.g1_neg(
+        B._smul(B.g1_add, B.G1_GEN, B.X_ABS * B.X_ABS))
+    for _ in range(2):
+        p = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+        q = B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))
+        assert B.g1_in_subgroup(p) and B.g1_endo_test(p)
+        assert B.g2_in_subgroup(q) and B.g2_endo_test(q)
+    for seed in (1, 0x5EED):
+        p0, q0 = B.g1_curve_point(seed), B.g2_curve_point(seed)
+        t1, t2 = B._smul(B.g1_add, p0, B.R), B._smul(B.g2_add, q0, B.R)
+        p1 = B.g1_add(B.g1_mul(B.G1_GEN, 11), t1)
+        q1 = B.g2_add(B.g2_mul(B.G2_GEN, 13), t2)
+        for pt in (p0, p1):
+            assert B.g1_on_curve(pt)
+            assert not B.g1_in_subgroup(pt) and not B.g1_endo_test(pt)
+        for pt in (q0, q1):
+            assert B.g2_on_curve(pt)
+            assert not B.g2_in_subgroup(pt) and not B.g2_endo_test(pt)
+
+
+def test_c_restatement_rejects_points_outside_subgroup():
+    """oracle/bls_pairing.c (the CPU baseline) decodes points as the crate does,
+    [r] P == O included: an on-curve point outside the subgroup is invalid (2)."""
+    from oracle import bls_c
+    p0, q0 = B.g1_curve_point(0x5EED), B.g2_curve_point(0x5EED)
+    G, Q = B.g1_bytes(B.g1_mul(B.G1_GEN, 5)), B.g2_bytes(B.g2_mul(B.G2_GEN, 7))
+    items = [(G, Q, G, Q), (B.g1_bytes(p0), Q, G, Q), (G, B.g2_bytes(q0), G, Q),
+             (G, Q, B.g1_bytes(p0), Q), (G, Q, G, B.g2_bytes(q0))]
+    g1 = b"".join(a + c for a, b, c, d in items)
+    g2 = b"".join(b + d for a, b, c, d in items)
+    assert bls_c.check_batch(g1, g2, len(items), 1) == bytes([1, 2, 2, 2, 2])

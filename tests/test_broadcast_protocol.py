@@ -384,6 +384,34 @@ def test_lockstep_batched_decodes(backend):
         assert decodes >= outputs > 0 and decodes > launches > 0
 
 
+def test_deferred_decode_refuses_interleaved_messages():
+    """decode_sink is run_lockstep's contract: once compute_output
+    has filed a decode, another message before resolve_decodes is an error,
+    not a silent extra BroadcastDecoding fault; after the resolution the
+    instance proceeds as the reference's does."""
+    from hbbft_amd.broadcast import resolve_decodes
+    backend = _oracle_backend()
+    n, proposer = 4, 0
+    k, S = 2, 4
+    framed = (struct.pack(">I", 3) + b"Foo").ljust(k * S, b"\0")
+    shards = [bytearray(framed[i * S:(i + 1) * S]) for i in range(k)] + [bytearray(S) for _ in range(2)]
+    backend.Coding(k, 2).encode(shards)
+    tree = backend.MerkleTree.from_vec([bytes(s) for s in shards])
+    node = Broadcast(3, range(n), proposer, backend=backend)
+    node.decode_sink = sink = []
+    for i in range(3):
+        node.handle_message(i, Message.echo(tree.proof(i)))
+    i = 0
+    while not sink:   # N - f Echoes sent our Ready; > 2f Readys file the decode
+        node.handle_message(i, Message.ready(tree.root_hash()))
+        i += 1
+    assert len(sink) == 1 and not node.terminated()
+    with pytest.raises(RuntimeError):
+        node.handle_message(i, Message.ready(tree.root_hash()))
+    ((bc, step),) = resolve_decodes(sink, backend)
+    assert bc is node and step.output == [b"Foo"] and node.terminated()
+
+
 def _epoch_value(n, p):
     # ragged contributions: several proposers share a length (one batch), one
     # is empty, the rest differ

@@ -201,3 +201,60 @@ def test_prepared_checks_match_plain_checks():
     # indices past the table (as uint32: -1 is 2^32-1) are invalid inputs, not reads
     ib2 = torch.tensor([0, 3, -1, 0], dtype=torch.int32, device="cuda:0")
     assert T.pairing_check_prepared(g1, prep, 3, ib2, idd).cpu().tolist() == [1, 2, 2, 1]
+
+
+def _off_subgroup_points():
+    """On-curve points outside the order-r subgroups (the crate's into_affine
+    rejects them): a plain curve point of E / E', and a subgroup point plus a
+    point of cofactor order ([r] of a curve point)."""
+    p0, q0 = B.g1_curve_point(0x5EED), B.g2_curve_point(0x5EED)
+    t1, t2 = B._smul(B.g1_add, p0, B.R), B._smul(B.g2_add, q0, B.R)
+    p1 = B.g1_add(B.g1_mul(B.G1_GEN, 11), t1)
+    q1 = B.g2_add(B.g2_mul(B.G2_GEN, 13), t2)
+    for pt in (p0, p1):
+        assert B.g1_on_curve(pt) and not B.g1_in_subgroup(pt)
+    for pt in (q0, q1):
+        assert B.g2_on_curve(pt) and not B.g2_in_subgroup(pt)
+    return [p0, p1], [q0, q1]
+
+
+@pytest.mark.parametrize("multi", ["1", "0"])
+def test_points_outside_subgroup_are_invalid(monkeypatch, multi):
+    """a point on the curve but outside the order-r subgroup (e.g.
+    share + T, T of cofactor order) is an invalid input (status / outcome 2)
+    in every form -- GT values, plain and multi-Miller checks, prepared G2
+    points and the G1 points checked against them -- as the crate's
+    deserialisation rejects it before any pairing."""
+    import torch
+    from hbbft_amd import threshold as T
+    monkeypatch.setenv("HBRBC_PAIR_MULTI", multi)
+    (p0, p1), (q0, q1) = _off_subgroup_points()
+    G, Q = B.g1_bytes(B.g1_mul(B.G1_GEN, 5)), B.g2_bytes(B.g2_mul(B.G2_GEN, 7))
+    one = B.gt_bytes(B.F12_ONE)
+    rows = [(G, Q, 0), (B.g1_bytes(p0), Q, 2), (B.g1_bytes(p1), Q, 2), (G, B.g2_bytes(q0), 2),
+            (G, B.g2_bytes(q1), 2)]
+    gt, st = T.pairing_batch(_t([r[0] for r in rows], 96), _t([r[1] for r in rows], 192))
+    assert st.cpu().tolist() == [r[2] for r in rows]
+    for i in range(1, len(rows)):
+        assert bytes(gt[i].cpu().numpy()) == one
+    # checks e(a, b) == e(c, d): a valid pair, then one bad point in each slot
+    good = (G, Q, G, Q)
+    cases = [good]
+    for slot, pt in ((0, B.g1_bytes(p1)), (1, B.g2_bytes(q1)), (2, B.g1_bytes(p0)),
+                     (3, B.g2_bytes(q0))):
+        c = list(good)
+        c[slot] = pt
+        cases.append(tuple(c))
+    g1 = _t([x for a, b, c, d in cases for x in (a, c)], 96)
+    g2 = _t([x for a, b, c, d in cases for x in (b, d)], 192)
+    assert T.pairing_check_batch(g1, g2).cpu().tolist() == [1, 2, 2, 2, 2]
+    # prepared: an off-subgroup G2 point is flagged at preparation, an
+    # off-subgroup share when its check runs
+    prep = T.g2_prepare(_t([Q, B.g2_bytes(q1)], 192))
+    g1 = _t([G, G, G, G, B.g1_bytes(p1), G], 96)
+    ib = torch.tensor([0, 1, 0], dtype=torch.int32, device="cuda:0")
+    idd = torch.tensor([0, 0, 0], dtype=torch.int32, device="cuda:0")
+    assert T.pairing_check_prepared(g1, prep, 2, ib, idd).cpu().tolist() == [1, 2, 2]
+    # the helpers hbbft's callers use return False for such a share
+    # (items are (share, pk_i, H, W): e(share, H) == e(pk_i, W))
+    assert T.verify_decryption_shares([(B.g1_bytes(p1), G, Q, Q), (G, G, Q, Q)]) == [False, True]

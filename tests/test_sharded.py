@@ -91,6 +91,19 @@ def _gloo_worker(rank, world, port, n, count, plen, q):
                 sh = shards_of(s, i)
                 for j in range(n):
                     assert torch.equal(blocked_row(echo, j, s * count + i, R, S), sh[j])
+        # the async form the pipelined schedule uses (handles waited after
+        # every collective of a group is issued) gives the same bytes, and the
+        # per-collective byte counts are what this rank sends
+        ex.reset_stats()
+        recv2, echo2 = torch.empty_like(recv), torch.empty_like(echo)
+        hs = [ex.all_to_all(recv2, slab, async_op=True, name="value_shards"),
+              ex.all_gather(echo2, recv, async_op=True, name="echo_shards")]
+        for h in hs:
+            h.wait()
+        assert torch.equal(recv2, recv) and torch.equal(echo2, echo)
+        nb = slab.numel()
+        assert ex.stats == {"value_shards": {"calls": 1, "bytes_sent": nb * (world - 1) // world},
+                            "echo_shards": {"calls": 1, "bytes_sent": nb * (world - 1)}}, ex.stats
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))
