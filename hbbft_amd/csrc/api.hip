@@ -2091,4 +2091,26 @@ int hbrbc_pairing_check(const uint8_t a[96], const uint8_t b[192], const uint8_t
     return HBRBC_OK;
 }
 
+// ---- f2: the Broadcast state machine, batched (sim.hip) -------------------
+size_t hbrbc_sm_state_bytes(size_t n, size_t roots) { return sm_state_bytes(n, roots); }
+
+int hbrbc_sm_round(hbrbc_ctx *c, const hbrbc_sm_args *a, void *stream) {
+    if (!c || !a) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    if (a->count == 0 || a->nodes == 0) return HBRBC_OK;
+    const size_t n = c->n;
+    if (n > 255) return fail(HBRBC_E_INVALID_ARG, "the state machine handles n <= 255 validators");
+    if (a->roots == 0 || a->roots > 8) return fail(HBRBC_E_INVALID_ARG, "roots must be 1..8");
+    if (a->max_out == 0 || a->rows_per_rank == 0 || a->node_lo >= n)
+        return fail(HBRBC_E_INVALID_ARG, "bad max_out / rows_per_rank / node_lo");
+    if (!a->proposer || !a->role || !a->value_root || !a->value_tamper || !a->proof_ok ||
+        !a->decode_ok || !a->fake_from || !a->fake_root || !a->fake_list || !a->out ||
+        !a->out_count || !a->state || !a->output_root || !a->fault_count || !a->emitted ||
+        (a->max_faults && !a->faults) || (a->round > 0 && (!a->in || !a->in_count)))
+        return fail(HBRBC_E_INVALID_ARG, "null argument");
+    HB_HIP(hipSetDevice(c->device));
+    const int f = (int)((n - c->k) / 2);
+    HB_HIP(launch_sm_round(*a, (int)n, f, (int)c->k, pick(c, stream)));
+    return HBRBC_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,320 @@
+"""The Reliable-Broadcast state machine of many instances and nodes on the GPU
+(SURVEY.md §8 row f2), sharded over ranks like the validator-sharded
+simulation (hbbft_amd/sharded.py).
+
+Control plane.  `hbrbc_sm_round` (hbbft_amd/csrc/sim.hip) runs
+/root/reference/src/broadcast/broadcast.rs:228-558 -- handle_value,
+handle_echo, handle_echo_hash, handle_can_decode, handle_ready, the senders
+and compute_output -- for every hosted (instance, node) in synchronous rounds:
+what a node emits in round t is delivered in round t + 1, handled in (sender,
+emission) order.  Every node's Echo / EchoHash / Ready / CanDecode state and
+counters live on the GPU; each round's messages (records of kind, root, proof
+index, tamper flag and an N-bit recipient mask) are all-gathered between the
+ranks (`StateMachineRank.exchange`), the Ready/EchoHash/CanDecode fan-out of
+SURVEY §5.
+
+Data plane.  Messages carry proofs by reference (root slot c, index j,
+tampered copy or not).  `data_plane` encodes each instance's codewords
+(send_shards_batch), validates every proof and its tampered copy
+(validate_proofs) and decodes each root once (decode_shards_batch): Proof::
+validate is a pure function of the proof, and a codeword decodes from any k
+of its rows, so the state machine looks the outcomes up (broadcast.rs:254,
+291, 551-557).
+
+Scenarios (`Scenario`): a proposer that sends different codewords, tampered
+proofs or nothing to some validators; faulty nodes that drop what they would
+send (tests/broadcast.rs:33-98 ProposeAdversary with drop), corrupt or
+withhold their Echoes; and the ProposeAdversary's injected broadcasts of the
+faulty nodes' own value.  tests/test_rbc_sim.py checks every node's output and
+fault log against the host restatement (hbbft_amd/broadcast.py driven by
+tests/virtual_net.py RoundNet) on the same scenarios.
+"""
+import ctypes
+
+import torch
+
+from . import _check, decode_shards_batch, lib, send_shards_batch, validate_proofs
+from . import RbcBatch
+
+NONE = 0xFF
+HONEST, SILENT, CORRUPT_ECHO, WITHHOLD_ECHO = 0, 1, 2, 3
+# FaultKind (broadcast/error.rs:28-50), in declaration order
+FAULT_KINDS = ["ReceivedValueFromNonProposer", "MultipleValues", "MultipleEchos",
+               "MultipleEchoHashes", "MultipleReadys", "InvalidProof", "BroadcastDecoding"]
+MSG_KINDS = ["Value", "Echo", "Ready", "CanDecode", "EchoHash", "Fake"]
+
+_P = ctypes.c_void_p
+
+
+class SmArgs(ctypes.Structure):
+    """struct hbrbc_sm_args (include/hbrbc.h)."""
+    _fields_ = [("count", ctypes.c_size_t), ("node_lo", ctypes.c_uint32),
+                ("nodes", ctypes.c_uint32), ("rows_per_rank", ctypes.c_uint32),
+                ("roots", ctypes.c_uint32), ("max_out", ctypes.c_uint32),
+                ("max_faults", ctypes.c_uint32), ("round", ctypes.c_int32)] + [
+        (name, _P) for name in (
+            "proposer", "role", "value_root", "value_tamper", "proof_ok", "decode_ok",
+            "fake_from", "fake_root", "fake_list", "in_", "in_count", "out", "out_count",
+            "state", "output_root", "faults", "fault_count", "emitted")]
+
+
+def _bind():
+    L = lib()
+    if not getattr(L, "_sm_bound", False):
+        L.hbrbc_sm_state_bytes.restype = ctypes.c_size_t
+        L.hbrbc_sm_state_bytes.argtypes = [ctypes.c_size_t, ctypes.c_size_t]
+        L.hbrbc_sm_round.restype = ctypes.c_int
+        L.hbrbc_sm_round.argtypes = [_P, ctypes.POINTER(SmArgs), _P]
+        L._sm_bound = True
+    return L
+
+
+# ------------------------------------------------------------------ scenario --
+class Instance:
+    """One broadcast instance: `values[c]` is the payload of root slot c (c = 0
+    the proposer's value); value_root[j] / value_tamper[j] what the proposer's
+    Value to node j carries (NONE: no Value); role[j] the node's behaviour;
+    fake_from (or None) the node that injects the broadcasts of the nodes in
+    fake_list, whose value is values[fake_root]."""
+
+    def __init__(self, n, proposer, values, value_root=None, value_tamper=None, role=None,
+                 fake_from=None, fake_list=(), fake_root=None):
+        self.n, self.proposer, self.values = n, proposer, [bytes(v) for v in values]
+        assert len(set(self.values)) == len(self.values), "root slots need distinct values"
+        self.value_root = list(value_root) if value_root is not None else [0] * n
+        self.value_tamper = list(value_tamper) if value_tamper is not None else [0] * n
+        self.role = list(role) if role is not None else [HONEST] * n
+        self.fake_from, self.fake_list, self.fake_root = fake_from, sorted(fake_list), fake_root
+        assert self.value_root[proposer] != NONE, "the proposer handles its own Value"
+        if fake_from is not None:
+            assert fake_root is not None and fake_list
+
+
+class Scenario:
+    """`count` instances of one validator count n (roots: codeword slots)."""
+
+    def __init__(self, n, instances):
+        self.n = n
+        self.instances = list(instances)
+        assert all(i.n == n for i in self.instances)
+        self.roots = max(len(i.values) for i in self.instances)
+        assert self.roots <= 8
+
+    @property
+    def count(self):
+        return len(self.instances)
+
+    def tensors(self, device):
+        n, cnt = self.n, self.count
+        W = (n + 31) // 32
+        u8 = dict(dtype=torch.uint8)
+        prop = torch.tensor([i.proposer for i in self.instances], **u8)
+        role = torch.tensor([i.role for i in self.instances], **u8).view(cnt, n)
+        vr = torch.tensor([i.value_root for i in self.instances], **u8).view(cnt, n)
+        vt = torch.tensor([i.value_tamper for i in self.instances], **u8).view(cnt, n)
+        ff = torch.tensor([NONE if i.fake_from is None else i.fake_from for i in self.instances], **u8)
+        fr = torch.tensor([0 if i.fake_root is None else i.fake_root for i in self.instances], **u8)
+        import numpy as np
+        flw = np.zeros((cnt, W), np.uint32)
+        for r, i in enumerate(self.instances):
+            for F in i.fake_list:
+                flw[r, F // 32] |= np.uint32(1 << (F % 32))
+        fl = torch.from_numpy(flw.view(np.int32))   # bit patterns (uint32 words)
+        return {k: v.to(device) for k, v in dict(proposer=prop, role=role, value_root=vr,
+                                                value_tamper=vt, fake_from=ff, fake_root=fr,
+                                                fake_list=fl).items()}
+
+
+def tampered(p):
+    """The corrupted copy of a proof a CORRUPT_ECHO node (or a tampering
+    proposer) sends: first value byte flipped, index / digests / root kept."""
+    v = p.value()
+    return type(p)(bytes([v[0] ^ 1]) + v[1:], p.index(), p.digests(), p.root_hash())
+
+
+def data_plane(scn, device=0):
+    """Encode every root slot's codeword (one batched launch per stage),
+    validate every proof and its tampered copy, decode each root once.
+    Returns proof_ok [count][roots][2][n], decode_ok [count][roots] (uint8,
+    on `device`), the decoded payloads {(inst, c): bytes} and the trees."""
+    n, cnt, C = scn.n, scn.count, scn.roots
+    items, keys = [], []
+    for r, inst in enumerate(scn.instances):
+        for c, v in enumerate(inst.values):
+            items.append((n, v))
+            keys.append((r, c))
+    trees = dict(zip(keys, send_shards_batch(items, device=device)))
+    proofs = {}
+    for (r, c), t in trees.items():
+        for j in range(n):
+            p = t.proof(j)
+            proofs[(r, c, 0, j)] = p
+            proofs[(r, c, 1, j)] = tampered(p)
+    validate_proofs(list(proofs.values()), n, device=device)
+    ok = torch.zeros((cnt, C, 2, n), dtype=torch.uint8)
+    for (r, c, t, j), p in proofs.items():
+        ok[r, c, t, j] = 1 if p.validate(n) else 0
+    # decode_from_shards of each root from n - f of its rows (a codeword
+    # decodes from any k of its rows; the last f are dropped so the
+    # reconstruct runs)
+    f = (n - 1) // 3
+    reqs = [(n, [v if j < n - f else None for j, v in enumerate(t.values())], t.root_hash())
+            for t in trees.values()]
+    outs = decode_shards_batch(reqs, device=device)
+    dec = torch.zeros((cnt, C), dtype=torch.uint8)
+    payloads = {}
+    for key, o in zip(trees, outs):
+        if o is not None:
+            dec[key] = 1
+            payloads[key] = o
+    return ok.to(device), dec.to(device), payloads, trees
+
+
+# ------------------------------------------------------------- one rank -----
+class StateMachineRank:
+    """The hosted nodes [node_lo, node_lo + R) of rank `rank` of `world` for
+    every instance of a scenario (R = ceil(n / world))."""
+
+    def __init__(self, scn, rank, world, device=0, max_out=24, max_faults=32, ok=None,
+                 dec=None):
+        self.scn, self.rank, self.world = scn, rank, world
+        n, cnt = scn.n, scn.count
+        self.n, self.count = n, cnt
+        self.R = -(-n // world)
+        self.node_lo = rank * self.R
+        self.W = (n + 31) // 32
+        self.rec = 1 + self.W
+        self.max_out, self.max_faults = max_out, max_faults
+        self.rb = RbcBatch(n, device=device)
+        dev = self.rb.device
+        self.device = dev
+        L = _bind()
+        sb = L.hbrbc_sm_state_bytes(n, scn.roots)
+        R = self.R
+        self.sc = scn.tensors(dev)
+        self.ok, self.dec = ok, dec
+        self.state = torch.zeros((cnt, R, sb), dtype=torch.uint8, device=dev)
+        self.out = torch.zeros((cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
+        self.out_count = torch.zeros((cnt, R), dtype=torch.int32, device=dev)
+        self.output_root = torch.full((cnt, R), NONE, dtype=torch.uint8, device=dev)
+        self.faults = torch.zeros((cnt, R, max(1, max_faults)), dtype=torch.int16, device=dev)
+        self.fault_count = torch.zeros((cnt, R), dtype=torch.int32, device=dev)
+        self.emitted = torch.zeros(1, dtype=torch.int32, device=dev)
+        # every sender's records of the previous round, [G][count][R][E][rec]
+        self.inbox = torch.zeros((world, cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
+        self.inbox_count = torch.zeros((world, cnt, R), dtype=torch.int32, device=dev)
+
+    def round(self, r, stream=None):
+        """Handle round r's inbox (round 0: the proposers' broadcast())."""
+        s = self.sc
+        a = SmArgs(count=self.count, node_lo=self.node_lo, nodes=self.R, rows_per_rank=self.R,
+                   roots=self.scn.roots, max_out=self.max_out, max_faults=self.max_faults, round=r)
+        for name in ("proposer", "role", "value_root", "value_tamper", "fake_from", "fake_root",
+                     "fake_list"):
+            setattr(a, name, s[name].data_ptr())
+        a.proof_ok, a.decode_ok = self.ok.data_ptr(), self.dec.data_ptr()
+        a.in_, a.in_count = self.inbox.data_ptr(), self.inbox_count.data_ptr()
+        a.out, a.out_count = self.out.data_ptr(), self.out_count.data_ptr()
+        a.state, a.output_root = self.state.data_ptr(), self.output_root.data_ptr()
+        a.faults, a.fault_count = self.faults.data_ptr(), self.fault_count.data_ptr()
+        a.emitted = self.emitted.data_ptr()
+        self.emitted.zero_()
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(_bind().hbrbc_sm_round(self.rb.coding.handle, ctypes.byref(a),
+                                      ctypes.c_void_p(st.cuda_stream)))
+
+    def check_overflow(self):
+        if bool((self.out_count < 0).any()):   # bit 31: more than max_out records
+            raise RuntimeError("state machine: a node emitted more than %d messages in a round"
+                               % self.max_out)
+
+    def exchange(self, ex, async_op=False):
+        """All-gather of this round's records (the Ready / EchoHash / CanDecode
+        and Echo-reference fan-out) into every rank's inbox."""
+        return [ex.all_gather(self.inbox, self.out, async_op, name="sm_messages"),
+                ex.all_gather(self.inbox_count, self.out_count, async_op, name="sm_counts")]
+
+    # -- results -------------------------------------------------------------
+    def outputs(self):
+        """[count][hosted] decided root slot or NONE."""
+        return self.output_root.cpu().numpy()
+
+    def fault_logs(self):
+        """{(inst, node): [(blamed node, FaultKind name)]} of the hosted nodes."""
+        fc = self.fault_count.cpu().numpy()
+        fl = self.faults.cpu().numpy().astype("uint16")
+        out = {}
+        for i in range(self.count):
+            for r in range(self.R):
+                node = self.node_lo + r
+                if node >= self.n:
+                    continue
+                cnt = int(fc[i, r])
+                if cnt > self.max_faults:
+                    raise RuntimeError("fault log overflow at (%d, %d): %d records" % (i, node, cnt))
+                out[(i, node)] = [(int(v) >> 8, FAULT_KINDS[int(v) & 0xFF]) for v in fl[i, r, :cnt]]
+        return out
+
+
+class LoopbackExchange:
+    """The all-gather of `world` virtual ranks living in one process."""
+
+    def __init__(self, ranks):
+        self.ranks = ranks
+
+    def gather(self):
+        outs = torch.stack([r.out for r in self.ranks])
+        cnts = torch.stack([r.out_count for r in self.ranks])
+        for r in self.ranks:
+            r.inbox.copy_(outs)
+            r.inbox_count.copy_(cnts)
+
+
+def run_rounds(ranks, exchange=None, max_rounds=64):
+    """Drive the state machine until no node emits a message.  `ranks`: the
+    StateMachineRank objects of this process (all of them for a loopback
+    run, one with a DistExchange `exchange`).  Returns the number of rounds."""
+    import torch.distributed as dist
+    loop = LoopbackExchange(ranks) if exchange is None else None
+    for r in range(max_rounds):
+        for sm in ranks:
+            sm.round(r)
+        for sm in ranks:
+            sm.check_overflow()
+        emitted = sum(int(sm.emitted.item()) for sm in ranks)
+        if exchange is not None and exchange.world > 1:
+            t = torch.tensor([emitted], dtype=torch.int64, device=ranks[0].device)
+            if exchange.staged:
+                t = t.cpu()
+            dist.all_reduce(t, group=exchange.group)
+            emitted = int(t.item())
+        if emitted == 0:
+            return r + 1
+        if loop is not None:
+            loop.gather()
+        else:
+            for h in ranks[0].exchange(exchange):
+                if h is not None:
+                    h.wait()
+    raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
+
+
+def simulate(scn, world=1, device=0, max_out=24, max_faults=32):
+    """Every node of every instance of `scn` over `world` virtual ranks on one
+    GPU.  Returns ({(inst, node): output bytes or None}, {(inst, node): fault
+    list}, rounds)."""
+    ok, dec, payloads, _ = data_plane(scn, device)
+    ranks = [StateMachineRank(scn, g, world, device, max_out, max_faults, ok, dec)
+             for g in range(world)]
+    rounds = run_rounds(ranks)
+    outputs, faults = {}, {}
+    for sm in ranks:
+        oc = sm.outputs()
+        for i in range(scn.count):
+            for r in range(sm.R):
+                node = sm.node_lo + r
+                if node < scn.n:
+                    c = int(oc[i, r])
+                    outputs[(i, node)] = None if c == NONE else payloads[(i, c)]
+        faults.update(sm.fault_logs())
+    return outputs, faults, rounds

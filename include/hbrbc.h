@@ -412,8 +412,9 @@ int hbrbc_unframe_fused(const hbrbc_ctx *ctx, size_t shard_len, size_t payload_s
  * Points use the crate's uncompressed encodings: G1 = 96 bytes x || y, G2 =
  * 192 bytes x.c1 || x.c0 || y.c1 || y.c0, big-endian, infinity = flag 0x40 in
  * byte 0 with every other bit zero.  Non-canonical coordinates (>= p), set
- * compression/sort flags and points off the curve are rejected per item;
- * subgroup membership is assumed (the crate's deserialisation checks it).
+ * compression/sort flags, points off the curve and points outside the
+ * order-r subgroup are rejected per item, as the crate's deserialisation
+ * (`into_affine`) rejects them.
  * hash_g1_g2 (SHA3 + ChaCha-seeded G2 sampling, once per ciphertext) stays
  * with the caller, which passes the G2 point. */
 #define HBRBC_G1_BYTES 96
@@ -457,6 +458,60 @@ int hbrbc_pairing_check_prepared(const uint8_t *g1, const void *prepared, size_t
  * invalid point. */
 int hbrbc_pairing_check(const uint8_t a[96], const uint8_t b[192], const uint8_t c[96],
                         const uint8_t d[192], int *result);
+
+/* ---- the Broadcast state machine, batched --------------- */
+/* Many instances x nodes of `Broadcast` (broadcast.rs:228-558) in synchronous
+ * rounds: what a node emits in round t is delivered in round t + 1, each node
+ * handling its inbox in (sender index, emission order).  Round 0 is the
+ * proposers' broadcast().  A message is a record of 1 + W uint32 words
+ * (W = ceil(n / 32)): word 0 = kind | root << 8 | index << 16 | tampered << 24
+ * (kind: 0 Value, 1 Echo, 2 Ready, 3 CanDecode, 4 EchoHash, 5 the
+ * ProposeAdversary's injected broadcasts), words 1..W = recipient bits.
+ * Proofs travel by reference (root c = codeword slot of the instance, index
+ * j, tampered copy or not): proof_ok holds Proof::validate of each (the
+ * batched validate kernel), decode_ok decode_from_shards of each root (the
+ * batched decode).  Nodes [node_lo, node_lo + nodes) are hosted here; the
+ * previous round's records of every sender s sit in `in` at block s / R, row
+ * s % R ([G][count][R][max_out][1 + W]); this round's go to `out`
+ * ([count][nodes][max_out][1 + W]); out_count bit 31 flags an overflow.
+ * Fault records: blamed node << 8 | FaultKind (error.rs:28-50 order). */
+#define HBRBC_SM_NONE 0xFF
+enum hbrbc_sm_role {            /* per instance and node */
+    HBRBC_SM_HONEST = 0,
+    HBRBC_SM_SILENT = 1,        /* emits nothing when handling a message (ProposeAdversary drop) */
+    HBRBC_SM_CORRUPT_ECHO = 2,  /* its Echoes carry the tampered copy of its proof */
+    HBRBC_SM_WITHHOLD_ECHO = 3  /* sends no Echo at all */
+};
+typedef struct hbrbc_sm_args {
+    size_t count;                 /* instances */
+    uint32_t node_lo, nodes;      /* hosted nodes */
+    uint32_t rows_per_rank;       /* R of the `in` layout (n for one rank) */
+    uint32_t roots;               /* codeword slots per instance, <= 8 */
+    uint32_t max_out;             /* records per node per round */
+    uint32_t max_faults;          /* fault records kept per node */
+    int32_t round;
+    const uint8_t *proposer;      /* [count] */
+    const uint8_t *role;          /* [count][n] */
+    const uint8_t *value_root;    /* [count][n]: root of the proposer's Value to node j, or NONE */
+    const uint8_t *value_tamper;  /* [count][n]: that Value carries the tampered copy */
+    const uint8_t *proof_ok;      /* [count][roots][2][n] */
+    const uint8_t *decode_ok;     /* [count][roots] */
+    const uint8_t *fake_from;     /* [count]: dispatcher of the injected broadcasts, or NONE */
+    const uint8_t *fake_root;     /* [count]: their codeword slot */
+    const uint32_t *fake_list;    /* [count][W]: the faulty nodes whose broadcasts are injected */
+    const uint32_t *in;
+    const uint32_t *in_count;     /* [G][count][R] */
+    uint32_t *out;
+    uint32_t *out_count;          /* [count][nodes] */
+    uint8_t *state;               /* [count][nodes][hbrbc_sm_state_bytes], zeroed before round 0 */
+    uint8_t *output_root;         /* [count][nodes]: decided root, NONE before */
+    uint16_t *faults;             /* [count][nodes][max_faults] */
+    uint32_t *fault_count;        /* [count][nodes] (may exceed max_faults) */
+    uint32_t *emitted;            /* += records emitted this round */
+} hbrbc_sm_args;
+size_t hbrbc_sm_state_bytes(size_t n, size_t roots);
+/* One round for the hosted nodes of every instance (ctx gives n, f, k). */
+int hbrbc_sm_round(hbrbc_ctx *ctx, const hbrbc_sm_args *args, void *stream);
 
 #ifdef __cplusplus
 }

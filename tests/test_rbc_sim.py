@@ -1,0 +1,237 @@
+"""the Broadcast state machine on the GPU (hbbft_amd/rbc_sim.py,
+hbbft_amd/csrc/sim.hip) under the reference's adversaries.
+
+Every scenario runs twice: through the GPU state machine (every node of every
+instance, Echo/EchoHash/Ready/CanDecode counters on the device, over 1..8
+virtual ranks whose per-round messages are all-gathered) and through the host
+restatement -- hbbft_amd/broadcast.py nodes driven round by round by
+tests/virtual_net.py run_rounds on the CPU oracle backend.  Every node's
+outputs, fault log (blamed node and FaultKind, in order) and the round count
+must be equal.
+
+Adversaries: tests/broadcast.rs:33-98 ProposeAdversary (the first f nodes
+inject their own "Fake news" broadcasts, with and without dropping everything
+else they send), a proposer sending two codewords / tampered proofs / nothing
+to different validators, faulty validators corrupting or withholding their
+Echoes, and mixtures of these.
+"""
+import os
+import random
+import socket
+
+import pytest
+import torch
+
+import virtual_net as vn
+from hbbft_amd.rbc_sim import (CORRUPT_ECHO, HONEST, NONE, SILENT, WITHHOLD_ECHO, Instance,
+                               Scenario)
+
+
+def _oracle():
+    import oracle_backend
+    return oracle_backend
+
+
+def _faulty(n):
+    return list(range(vn.max_faulty(n)))
+
+
+KINDS = ("honest", "propose", "propose_drop", "equivocate", "equivocate_2of3", "corrupt_echo",
+         "withhold_echo", "partial_values", "tampered_values", "mixed")
+BAD_PROPOSER = ("equivocate", "equivocate_2of3", "partial_values", "tampered_values", "mixed")
+
+
+def make_instances(n, rng, seed_tag=0):
+    """Scenario instances of one validator count covering every adversary."""
+    f = vn.max_faulty(n)
+    out = []
+
+    def value(tag):
+        return b"%s-%d-%d-" % (tag, n, seed_tag) + bytes(rng.randrange(256) for _ in range(rng.randrange(0, 40)))
+
+    for kind in KINDS:
+        # a misbehaving proposer is one of the f faulty nodes (the first f), so
+        # at most f nodes misbehave and the reference's guarantees apply
+        bad_proposer = kind in BAD_PROPOSER
+        if bad_proposer and not f:
+            kind, bad_proposer = "honest", False
+        p = rng.randrange(f) if bad_proposer else rng.randrange(n)
+        vals = [value(b"A")]
+        role = [HONEST] * n
+        vr, vt = [0] * n, [0] * n
+        fake_from, fake_list, fake_root = None, (), None
+        if kind in ("propose", "propose_drop") and f:
+            vals.append(b"Fake news")
+            fake_list = _faulty(n)
+            cand = [F for F in fake_list if F != p]
+            fake_from = cand[0] if cand else p
+            fake_root = 1
+            if kind == "propose_drop":
+                for F in fake_list:
+                    role[F] = SILENT
+        elif kind.startswith("equivocate"):
+            vals.append(value(b"B"))
+            share = 2 if kind == "equivocate" else 3
+            for j in range(n):
+                vr[j] = 1 if (j + p) % share == 0 else 0
+            vr[p] = 0
+        elif kind == "corrupt_echo":
+            for F in _faulty(n):
+                role[F] = CORRUPT_ECHO
+        elif kind == "withhold_echo":
+            for F in _faulty(n):
+                role[F] = WITHHOLD_ECHO
+        elif kind == "partial_values":
+            for j in rng.sample(range(n), min(n - 1, f + 1)):
+                if j != p:
+                    vr[j] = NONE
+        elif kind == "tampered_values":
+            for j in rng.sample(range(n), min(n, f + 1)):
+                vt[j] = 1
+        elif kind == "mixed" and f:
+            vals.append(value(b"B"))
+            vals.append(b"Fake news")
+            fake_list = _faulty(n)
+            fake_from, fake_root = fake_list[-1], 2
+            for j in range(n):
+                vr[j] = rng.choice([0, 0, 0, 1, NONE])
+                vt[j] = 1 if rng.random() < 0.1 else 0
+            vr[p], vt[p] = 0, 0
+            for F in fake_list:
+                role[F] = rng.choice([HONEST, SILENT, CORRUPT_ECHO, WITHHOLD_ECHO])
+        out.append(Instance(n, p, vals, vr, vt, role, fake_from, fake_list, fake_root))
+    return out
+
+
+def host_run(inst):
+    outs, faults, rounds = vn.run_rounds(inst, _oracle())
+    return outs, faults, rounds
+
+
+# ------------------------------------------------------------------ CPU ----
+def test_round_schedule_honest_and_propose_adversary():
+    """The round driver itself reproduces the reference's test assertions
+    (tests/broadcast.rs:127-146): with a correct proposer every node outputs the
+    value exactly once; otherwise all correct nodes (index >= f) agree."""
+    rng = random.Random(3)
+    for n in (1, 2, 4, 7, 10):
+        f = vn.max_faulty(n)
+        for inst in make_instances(n, rng):
+            outs, faults, _ = host_run(inst)
+            honest_p = (inst.proposer >= f and all(v == 0 for v in inst.value_root)
+                        and not any(inst.value_tamper))
+            if honest_p:
+                assert all(outs[i] == [inst.values[0]] for i in range(n)), (n, outs)
+            else:
+                assert len({tuple(outs[i]) for i in range(f, n)}) == 1, (n, outs)
+            # a correct node never blames a correct one
+            for i in range(f, n):
+                assert all(b < f or (b == inst.proposer and not honest_p) for b, _ in faults[i]), \
+                    (n, i, faults[i])
+
+
+def _gloo_sm_worker(rank, world, port, q):
+    """The state machine's per-round exchange shape: every rank's records
+    [count][R][E][1 + W] (and counts [count][R]) all-gathered into the
+    blocked inbox [G][count][R][E][1 + W] the kernel reads (sender s at block
+    s // R, row s % R)."""
+    import torch.distributed as dist
+
+    from hbbft_amd.sharded import DistExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, count, E = 10, 3, 4
+        R, rec = -(-n // world), 1 + (n + 31) // 32
+        out = torch.zeros((count, R, E, rec), dtype=torch.int32)
+        cnt = torch.zeros((count, R), dtype=torch.int32)
+        for i in range(count):
+            for r in range(R):
+                s = rank * R + r
+                cnt[i, r] = (s + i) % E
+                for e in range(E):
+                    out[i, r, e, 0] = s * 1000 + i * 10 + e
+        inbox = torch.empty((world, count, R, E, rec), dtype=torch.int32)
+        icnt = torch.empty((world, count, R), dtype=torch.int32)
+        ex = DistExchange()
+        for h in [ex.all_gather(inbox, out, True, name="sm_messages"),
+                  ex.all_gather(icnt, cnt, True, name="sm_counts")]:
+            h.wait()
+        good = True
+        for s in range(world * R):
+            for i in range(count):
+                blk = inbox[s // R, i, s % R]
+                good &= int(icnt[s // R, i, s % R]) == (s + i) % E
+                good &= [int(blk[e, 0]) for e in range(E)] == [s * 1000 + i * 10 + e for e in range(E)]
+        q.put((rank, "ok" if good else "mismatch"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_state_machine_exchange_shape():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_gloo_sm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: "ok", 1: "ok"}, res
+
+
+# ------------------------------------------------------------------ GPU ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,worlds", [(4, (1, 2)), (7, (1, 3)), (10, (1, 4)), (16, (1, 2, 8)),
+                                      (31, (1, 4)), (64, (8,))])
+def test_state_machine_matches_host_restatement(n, worlds):
+    """Per node: outputs, fault log (blamed node + kind, in order) and the
+    number of rounds equal the host state machine on the same schedule."""
+    from hbbft_amd.rbc_sim import simulate
+    rng = random.Random(1000 + n)
+    insts = make_instances(n, rng) + make_instances(n, rng, seed_tag=1)
+    if n == 64:
+        insts = insts[:10]
+    scn = Scenario(n, insts)
+    ref = [host_run(inst) for inst in insts]
+    for world in worlds:
+        outs, faults, rounds = simulate(scn, world=world)
+        assert rounds == max(r[2] for r in ref), (world, rounds, [r[2] for r in ref])
+        for i, (ho, hf, _) in enumerate(ref):
+            for node in range(n):
+                got = [] if outs[(i, node)] is None else [outs[(i, node)]]
+                assert got == ho[node], (world, i, node, got, ho[node])
+                assert faults[(i, node)] == hf[node], (world, i, node, faults[(i, node)], hf[node])
+
+
+@pytest.mark.gpu
+def test_state_machine_counters_at_size():
+    """4096 honest N=64 instances and 4096 ProposeAdversary-with-drop
+    instances on 8 virtual ranks: every correct node decides the proposer's
+    value (honest proposer), and the fault logs blame only faulty nodes."""
+    from hbbft_amd.rbc_sim import simulate
+    n, f = 64, 21
+    rng = random.Random(7)
+    insts = []
+    for i in range(256):
+        p = rng.randrange(f, n)          # a correct proposer
+        vals = [b"value %d" % i]
+        if i % 2:
+            role = [SILENT] * f + [HONEST] * (n - f)
+            insts.append(Instance(n, p, vals + [b"Fake news"], role=role, fake_from=0,
+                                  fake_list=range(f), fake_root=1))
+        else:
+            insts.append(Instance(n, p, vals))
+    outs, faults, rounds = simulate(Scenario(n, insts), world=8)
+    for i, inst in enumerate(insts):
+        for node in range(n):
+            assert outs[(i, node)] == inst.values[0]
+            assert all(b < f for b, _ in faults[(i, node)])
+    assert rounds <= 8

@@ -18,8 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from hbbft_amd.broadcast import (Broadcast, Message, broadcast_many, prevalidate,  # noqa: E402
-                                 resolve_decodes)
+from hbbft_amd.broadcast import (Broadcast, Message, Step, Target, TargetedMessage,  # noqa: E402
+                                 broadcast_many, prevalidate, resolve_decodes)
 
 
 class CrankError(AssertionError):
@@ -325,3 +325,99 @@ def broadcast_different_sizes(new_adversary, value, rng, backend, sizes=None):
                          new_adversary(), rng, message_limit=10_000 * size)
         nets.append(run_broadcast(net, value, proposer))
     return nets
+
+
+# ---- synchronous rounds (the schedule of the GPU state machine) -------------
+def codeword_tree(backend, n, value):
+    """send_shards (broadcast.rs:170-204) of `value` over n validators."""
+    f = max_faulty(n)
+    k, m = n - 2 * f, 2 * f
+    framed = len(value).to_bytes(4, "big") + bytes(value)
+    S = max(1, (len(framed) + k - 1) // k)
+    buf = framed.ljust(S * n, b"\0")
+    shards = [bytearray(buf[i * S:(i + 1) * S]) for i in range(n)]
+    backend.Coding(k, m).encode(shards)
+    return backend.MerkleTree.from_vec([bytes(s) for s in shards])
+
+
+def run_rounds(inst, backend, max_rounds=64):
+    """The host restatement of hbbft_amd/rbc_sim.py's schedule for one
+    scenario instance (hbbft_amd.rbc_sim.Instance): hbbft_amd/broadcast.py
+    nodes exchange messages in synchronous rounds -- what a node emits in
+    round t is delivered in round t + 1, each node handling its inbox in
+    (sender index, emission order).  Round 0 is the proposer's broadcast()
+    with its per-recipient Values (value_root / value_tamper).  Roles filter
+    what a node sends after handling a message: SILENT drops everything (the
+    ProposeAdversary with drop, tests/broadcast.rs:66-71), CORRUPT_ECHO
+    sends the tampered copy of every Echo proof, WITHHOLD_ECHO no Echo.  After
+    its first handled message, inst.fake_from sends the broadcasts of every
+    node in inst.fake_list (tests/broadcast.rs:73-97), unfiltered.
+    Returns ({node: [outputs]}, {node: [(blamed, FaultKind name)]}, rounds)."""
+    from hbbft_amd.rbc_sim import CORRUPT_ECHO, NONE, SILENT, WITHHOLD_ECHO, tampered
+    n, p = inst.n, inst.proposer
+    ids = list(range(n))
+    nodes = {i: Broadcast(i, ids, p, backend=backend) for i in ids}
+    outputs = {i: [] for i in ids}
+    faults = {i: [] for i in ids}
+    trees = [codeword_tree(backend, n, v) for v in inst.values]
+
+    def record(i, st):
+        outputs[i].extend(st.output)
+        faults[i].extend((fl.node_id, fl.kind.name) for fl in st.fault_log)
+
+    def sent(i, msgs, first_round=False):
+        role = inst.role[i]
+        if role == SILENT and not first_round:
+            return []
+        out = []
+        for tm in msgs:
+            if tm.message.kind == Message.ECHO:
+                if role == WITHHOLD_ECHO:
+                    continue
+                if role == CORRUPT_ECHO:
+                    tm = TargetedMessage(tm.target, Message.echo(tampered(tm.message.payload)))
+            out.append(tm)
+        return out
+
+    def proof(c, j, t):
+        pr = trees[c].proof(j)
+        return tampered(pr) if t else pr
+
+    # round 0: broadcast() with the scenario's Values (broadcast.rs:123-137, 212-222)
+    bc = nodes[p]
+    bc.value_sent = True
+    step = Step()
+    for j in ids:
+        if j != p and inst.value_root[j] != NONE:
+            step.messages.append(Target.node(j).message(
+                Message.value(proof(inst.value_root[j], j, inst.value_tamper[j]))))
+    step = step.join(bc._handle_value(p, proof(inst.value_root[p], p, inst.value_tamper[p])))
+    record(p, step)
+    outbox = {i: [] for i in ids}
+    outbox[p] = sent(p, step.messages, first_round=True)
+    fake_done = False
+    rounds = 1
+    while any(outbox.values()):
+        if rounds >= max_rounds:
+            raise CrankError("no quiescence in %d rounds" % max_rounds)
+        inbox = {r: [] for r in ids}
+        for s in ids:
+            for tm in outbox[s]:
+                for r in ids:
+                    if r != s and tm.target.contains(r):
+                        inbox[r].append((s, tm.message))
+        nxt = {i: [] for i in ids}
+        for r in ids:
+            for s, msg in inbox[r]:
+                st = nodes[r].handle_message(s, msg)
+                record(r, st)
+                nxt[r].extend(sent(r, st.messages))
+                if inst.fake_from == r and not fake_done:
+                    fake_done = True
+                    for F in inst.fake_list:
+                        fake = Broadcast(F, ids, F, backend=backend).handle_input(
+                            inst.values[inst.fake_root])
+                        nxt[r].extend(fake.messages)
+        outbox = nxt
+        rounds += 1
+    return outputs, faults, rounds
