@@ -665,6 +665,52 @@ int spec_sync() {
     return 0;
 }
 
+// LDS-staged specialised kernels (jit.hip gen_xor_kernel_lds): every input
+// transposed once per workgroup.  HBRBC_JIT_LDS=0/1 overrides (A/B).
+bool spec_lds() {
+    const char *e = getenv("HBRBC_JIT_LDS");
+    return e && !std::strcmp(e, "1");
+}
+
+// XOR-network form: 0 auto, 1 pairwise, 2 nibble-subset (HBRBC_JIT_NET, A/B).
+int spec_net() {
+    if (const char *e = getenv("HBRBC_JIT_NET")) return std::max(0, std::min(2, atoi(e)));
+    return 0;
+}
+
+// LDS stage size (inputs per stage) and waves/SIMD target of the LDS form
+// (HBRBC_JIT_LDS_STAGE, HBRBC_JIT_WPE; A/B).
+int spec_lds_stage() {
+    if (const char *e = getenv("HBRBC_JIT_LDS_STAGE")) return std::max(1, std::min(32, atoi(e)));
+    return 0;
+}
+int spec_wpe() {
+    if (const char *e = getenv("HBRBC_JIT_WPE")) return std::max(0, std::min(8, atoi(e)));
+    return 0;
+}
+
+// Code-object name suffix of the variant options above (only where they
+// change the generated code: the LDS form needs 2..8 passes).
+std::string spec_suffix(size_t nout, int rt) {
+    const int npass = (int)((nout + rt - 1) / rt);
+    std::string s;
+    if (spec_lds() && npass >= 2 && npass <= 8) {
+        s += "_L";
+        if (spec_lds_stage()) s += std::to_string(spec_lds_stage());
+    }
+    if (spec_net()) s += "_n" + std::to_string(spec_net());
+    if (spec_wpe()) s += "_w" + std::to_string(spec_wpe());
+    return s;
+}
+
+void spec_variant(XorProgram &p) {
+    p.lds = spec_lds();
+    p.lds_stage = spec_lds_stage();
+    p.net = spec_net();
+    p.wpe = spec_wpe();
+    p.name += spec_suffix(p.out_rows.size(), p.rt);
+}
+
 bool read_file(const std::string &path, std::vector<char> &out) {
     FILE *f = fopen(path.c_str(), "rb");
     if (!f) return false;
@@ -714,6 +760,7 @@ XorProgram encode_program(size_t k, size_t m, const uint8_t *parity_rows, int rt
     p.depth = depth;
     p.rb = rb;
     p.fused = true;
+    spec_variant(p);
     return p;
 }
 
@@ -745,6 +792,9 @@ bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const 
         p.guard = hash;
         p.uf_k = uf ? (int)k : 0;       // fused unframe: rebuilt data rows, and
         p.uf_inputs = uf && gi == 0;    // the present ones from the first program
+        if (uf) p.name.resize(p.name.size() - 3);   // variant suffix before "_uf"
+        spec_variant(p);
+        if (uf) p.name += "_uf";
         out.push_back(std::move(p));
     }
     return true;
@@ -1882,7 +1932,8 @@ int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t 
         jit_file("", encode_kernel_name(data_shards, parity_shards, rt, spec_depth(),
                                         groups[group].first, groups[group].second, rb,
                                         spec_sync(), spec_fdepth(), spec_spread(),
-                                        spec_split())).substr(1);
+                                        spec_split()) +
+                     spec_suffix(groups[group].second - groups[group].first, rt)).substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
     std::memcpy(buf, f.c_str(), f.size() + 1);
     return HBRBC_OK;

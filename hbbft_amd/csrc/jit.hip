@@ -247,32 +247,28 @@ void gen_pair_network(std::ostringstream &o, const CoefView &cv, int t0, int row
         }
 }
 
-// One kernel of a program: `fused` = the frame+encode twin.
-std::string gen_xor_kernel(const XorProgram &p, bool fused) {
-    const size_t nin = p.in_rows.size();
-    const int nout = (int)p.out_rows.size();
-    // npass passes of at most rt rows, balanced (42 rows at rt 12: 11, 11,
-    // 10, 10 rather than 12, 12, 12, 6 -- the longest pass sets the time)
-    const int npass = (nout + p.rt - 1) / p.rt;
-    auto pass_lo = [&](int ps) { return ps * (nout / npass) + std::min(ps, nout % npass); };
-    const int rt = (nout + npass - 1) / npass;
-    const int depth = fused ? p.fdepth : p.depth;  // 36 bytes per row in flight when fused
-    const int nbuf = depth + 1;
-    const int rb = p.rb;
-    // every wave runs exactly one pass only when npass <= 8 waves: only then
-    // do all waves reach the same barriers
-    const bool lockstep = p.sync > 0 && npass <= 8 && npass > 1;
-    const CoefView cv{p.coefs.data(), nin};
-    auto blk = [&](int row) { return row / rb; };
-    auto rin = [&](int row) { return row % rb; };
-    std::set<int> blocks;
-    for (int r : p.in_rows) blocks.insert(blk(r));
-    for (int r : p.out_rows) blocks.insert(blk(r));
-    std::ostringstream o;
+// Network of input jj for output rows t0..t0+rows-1 (net: 0 auto, 1 pairwise,
+// 2 nibble-subset).
+void gen_network(std::ostringstream &o, const CoefView &cv, int t0, int rows, size_t jj, int rt,
+                 int net) {
+    if (net == 2 || (net == 0 && rt <= 8))
+        gen_nibble_network(o, cv, t0, rows, jj);
+    else
+        gen_pair_network(o, cv, t0, rows, jj);
+}
+
+// Signature, guard, lane mapping, buffer resources and the load macros shared
+// by both kernel forms.  `fused` = the frame+encode twin.
+void gen_prologue(std::ostringstream &o, const XorProgram &p, bool fused, int npass,
+                  const std::set<int> &blocks, const char *d2, const std::string &lds_decl) {
+    auto blk = [&](int row) { return row / p.rb; };
+    (void)blk;
     // one wave per pass (up to 8): the waves of a workgroup stream the same
     // input rows together, so each row comes from HBM about once per program
     // (4 waves over 6 passes fetched 4.6x the input at cfg5, PMC FETCH_SIZE)
-    o << "\nextern \"C\" __global__ __launch_bounds__(" << xor_waves(npass) * 64 << ") void "
+    o << "\nextern \"C\" __global__ __launch_bounds__(" << xor_waves(npass) * 64 << ") "
+      << (p.wpe > 0 ? "__attribute__((amdgpu_waves_per_eu(" + std::to_string(p.wpe) + "))) " : std::string())
+      << "void "
       << p.name << (fused ? "_fe" : "")
       << "(uint8_t *__restrict__ base, unsigned long inst_stride, unsigned long shard_stride,\n"
          "    unsigned long block_stride, unsigned row_bytes, unsigned waves_per_row,\n"
@@ -280,7 +276,8 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
          "    const int *__restrict__ pat, const unsigned long *__restrict__ slot_hash, int hash_slots,\n"
          "    int p_only, uint8_t *__restrict__ uf_payload, unsigned long uf_stride,\n"
          "    const int *__restrict__ uf_status) {\n"
-         "  const unsigned long inst = blockIdx.x / waves_per_row;\n";
+      << lds_decl
+      << "  const unsigned long inst = blockIdx.x / waves_per_row;\n";
     if (p.guard) {
         // reconstruct of one cached erasure pattern: other patterns return
         char g[64];
@@ -293,7 +290,6 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
     // 32 consecutive bytes (off2 = off + 16); split: two 16-byte pieces 1 KB
     // apart, so every load and store instruction of a wave covers 1 KB of
     // consecutive bytes instead of 64 pieces of 16 with 16-byte gaps
-    const char *d2 = p.split ? "1024u" : "16u";
     o << "  const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);\n"
          "  const unsigned wchunk = blockIdx.x - (unsigned)inst * waves_per_row, lane = threadIdx.x & 63u;\n"
       << (p.split ? "  unsigned off = wchunk * 2048u + lane * 16u;\n" : "  unsigned off = (wchunk * 64u + lane) * 32u;\n")
@@ -346,6 +342,32 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
              "QA2 = __builtin_amdgcn_raw_buffer_load_b32(pr, a_ + 16u, 0, 0); "
              "QB = __builtin_amdgcn_raw_buffer_load_b128(pr, b_, 0, 0); "
              "QB2 = __builtin_amdgcn_raw_buffer_load_b32(pr, b_ + 16u, 0, 0); }\n";
+}
+
+// One kernel of a program: `fused` = the frame+encode twin.
+std::string gen_xor_kernel(const XorProgram &p, bool fused) {
+    const size_t nin = p.in_rows.size();
+    const int nout = (int)p.out_rows.size();
+    // npass passes of at most rt rows, balanced (42 rows at rt 12: 11, 11,
+    // 10, 10 rather than 12, 12, 12, 6 -- the longest pass sets the time)
+    const int npass = (nout + p.rt - 1) / p.rt;
+    auto pass_lo = [&](int ps) { return ps * (nout / npass) + std::min(ps, nout % npass); };
+    const int rt = (nout + npass - 1) / npass;
+    const int depth = fused ? p.fdepth : p.depth;  // 36 bytes per row in flight when fused
+    const int nbuf = depth + 1;
+    const int rb = p.rb;
+    // every wave runs exactly one pass only when npass <= 8 waves: only then
+    // do all waves reach the same barriers
+    const bool lockstep = p.sync > 0 && npass <= 8 && npass > 1;
+    const CoefView cv{p.coefs.data(), nin};
+    auto blk = [&](int row) { return row / rb; };
+    auto rin = [&](int row) { return row % rb; };
+    std::set<int> blocks;
+    for (int r : p.in_rows) blocks.insert(blk(r));
+    for (int r : p.out_rows) blocks.insert(blk(r));
+    const char *d2 = p.split ? "1024u" : "16u";
+    std::ostringstream o;
+    gen_prologue(o, p, fused, npass, blocks, d2, "");
 
     // p_only >= 0: this launch runs that one pass with one wave per workgroup
     // (the host launches the passes one after another, so every wave on a CU
@@ -436,10 +458,8 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
                       << "u, off2, x[4], x[5], x[6], x[7]); }\n";
                 o << "        hb_tr(x);\n";
             }
-            if (rt <= 8)   // short passes: the nibble-subset network
-                gen_nibble_network(o, cv, t0, rows, jj);
-            else
-                gen_pair_network(o, cv, t0, rows, jj);
+            // short passes: the nibble-subset network (net 0), or as forced
+            gen_network(o, cv, t0, rows, jj, rt, p.net);
             // pin the accumulators after every input: without this the
             // reassociation pass flattens each accumulator's whole XOR chain
             // over all inputs and keeps every input's planes live at once
@@ -468,6 +488,161 @@ std::string gen_xor_kernel(const XorProgram &p, bool fused) {
         o << "      }\n      break; }\n";
     }
     o << "    }\n  }\n}\n#undef HB_LD\n" << (fused ? "#undef HB_LDF\n#undef HB_LDF2\n" : "");
+    return o.str();
+}
+
+// LDS-staged form (p.lds): every input row of a stage is loaded, framed and
+// transposed ONCE per workgroup -- by wave jj % nw -- and its 8 bit planes go
+// to LDS ([jj][half][lane] u32x4: conflict-free 16-byte lane slots); after one
+// barrier every wave runs its pass over all inputs of the stage from LDS.  In
+// the streaming form each of the npass waves loads and transposes every input
+// itself (the transposes are ~25 % of a pass's VALU at cfg3) and keeps
+// depth + 1 rows of load buffers live beside its accumulators (231 VGPRs, 2
+// waves/SIMD); here a pass holds only its accumulators, 8 planes and the
+// network's temporaries.  Stages of <= 24 inputs (48 KB of LDS) bound the
+// LDS per workgroup; a barrier separates stages (the next stage's planes
+// overwrite the buffer).
+std::string gen_xor_kernel_lds(const XorProgram &p, bool fused) {
+    const int nin = (int)p.in_rows.size();
+    const int nout = (int)p.out_rows.size();
+    const int npass = (nout + p.rt - 1) / p.rt;
+    auto pass_lo = [&](int ps) { return ps * (nout / npass) + std::min(ps, nout % npass); };
+    const int rt = (nout + npass - 1) / npass;
+    const int nw = xor_waves(npass);
+    const int rb = p.rb;
+    const CoefView cv{p.coefs.data(), (size_t)nin};
+    auto blk = [&](int row) { return row / rb; };
+    auto rin = [&](int row) { return row % rb; };
+    std::set<int> blocks;
+    for (int r : p.in_rows) blocks.insert(blk(r));
+    for (int r : p.out_rows) blocks.insert(blk(r));
+    const char *d2 = p.split ? "1024u" : "16u";
+    const int ss = std::min(nin, p.lds_stage > 0 ? p.lds_stage : 24);
+    const int nstage = (nin + ss - 1) / ss;
+    std::ostringstream o;
+    gen_prologue(o, p, fused, npass, blocks, d2,
+                 "  __shared__ u32x4 hb_pl[" + std::to_string(ss) + "][2][64];\n");
+    if (fused)
+        // S through an opaque SGPR copy: otherwise the row offsets j * S - 4
+        // of every input are hoisted and kept live
+        o << "  unsigned S_; __asm__ volatile(\"s_mov_b32 %0, %1\" : \"=s\"(S_) : \"s\"(S));\n"
+             "  const unsigned Sx = S_;\n";
+    o << "  const int w_ = __builtin_amdgcn_readfirstlane(wave);\n"
+         "  switch (w_) {\n";
+    // one case per wave; a wave runs pass w_ (npass <= 8 = nw here) and
+    // loads the inputs jj of every stage with (jj - stage_lo) % nw == w_
+    for (int w = 0; w < nw; ++w) {
+        const bool has_pass = w < npass;
+        const int t0 = has_pass ? pass_lo(w) : 0;
+        const int rows = has_pass ? pass_lo(w + 1) - t0 : 0;
+        o << "  case " << w << ": {\n    __asm__ volatile(\"; wave " << w << "\" ::: \"memory\");\n";
+        if (fused) o << "    const unsigned S = Sx;\n";
+        if (rows) o << "    uint32_t a[" << rows << "][8] = {};\n";
+        for (int st = 0; st < nstage; ++st) {
+            const int lo = st * ss, hi = std::min(nin, lo + ss);
+            std::vector<int> mine;
+            for (int jj = lo; jj < hi; ++jj)
+                if ((jj - lo) % nw == w) mine.push_back(jj);
+            // phase 1: load (all of this wave's rows of the stage at once when
+            // no accumulators are live yet, else two ahead), frame, transpose
+            const int depth = (st == 0) ? (int)mine.size() : std::min<int>(2, (int)mine.size());
+            const int nbuf = std::max(1, depth + (st == 0 ? 0 : 1));
+            if (!mine.empty()) {
+                if (fused)
+                    o << "    { u32x4 q0[" << nbuf << "], q1[" << nbuf << "]; uint32_t q2[" << nbuf << "]"
+                      << (p.split ? ", q3[" + std::to_string(nbuf) + "]" : std::string()) << ";\n";
+                else
+                    o << "    { u32x4 l[" << nbuf << "], h[" << nbuf << "];\n";
+            }
+            auto load = [&](size_t m) {
+                const int b = (int)(m % nbuf);
+                const int row = p.in_rows[mine[m]];
+                if (fused && p.split)
+                    o << "      HB_LDF2(q0[" << b << "], q2[" << b << "], q1[" << b << "], q3[" << b << "], " << row << "u)";
+                else if (fused)
+                    o << "      HB_LDF(q0[" << b << "], q1[" << b << "], q2[" << b << "], " << row << "u)";
+                else
+                    o << "      HB_LD(l[" << b << "], h[" << b << "], " << blk(row) << ", " << rin(row) << "u)";
+                o << " __asm__ volatile(\"\" ::: \"memory\");\n";
+            };
+            for (int m = 0; m < depth; ++m) load((size_t)m);
+            for (size_t m = 0; m < mine.size(); ++m) {
+                const int jj = mine[m];
+                const int row = p.in_rows[jj];
+                const std::string c = std::to_string(m % nbuf);
+                if (m + depth < mine.size()) load(m + depth);
+                if (fused) {
+                    o << "      { uint32_t x[8];\n";
+                    if (p.split)
+                        o << "        hb_window2(q0[" << c << "], q2[" << c << "], q1[" << c << "], q3[" << c
+                          << "], (" << row << "u * S - 4u) & 3u, x);\n";
+                    else
+                        o << "        hb_window(q0[" << c << "], q1[" << c << "], q2[" << c << "], (" << row
+                          << "u * S - 4u) & 3u, x);\n";
+                    if (row < 4)
+                        o << "        if (" << row << "u * S < 4u) { if (off == 0u) "
+                          << (p.split ? "hb_frame_head2(q0[" + c + "], " : "hb_frame_head(q0[" + c + "], q1[" + c + "], ")
+                          << "P, " << row << "u * S, x); }\n";
+                    o << "        if (edge) {\n"
+                         "          _Pragma(\"unroll\") for (int i_ = 0; i_ < 8; ++i_) {\n"
+                         "            const int lim_ = (int)S - (int)(i_ < 4 ? off + 4 * i_ : off2 + 4 * (i_ - 4));\n"
+                         "            x[i_] = lim_ >= 4 ? x[i_] : (lim_ <= 0 ? 0u : x[i_] & (0xFFFFFFFFu >> (8 * (4 - lim_))));\n"
+                         "          }\n        }\n";
+                    // the first parity group writes the framed data rows
+                    if (p.out_rows.front() == nin)
+                        o << "        if (active) {\n"
+                             "          __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[0], x[1], x[2], x[3]}, rs"
+                          << blk(row) << ", off, " << rin(row) << "u * sst, HB_ST_AUX);\n"
+                             "          if (full) __builtin_amdgcn_raw_buffer_store_b128((u32x4){x[4], x[5], x[6], x[7]}, "
+                             "rs" << blk(row) << ", off2, " << rin(row) << "u * sst, HB_ST_AUX);\n        }\n";
+                } else {
+                    o << "      { const u32x4 hh = full ? h[" << c << "] : (u32x4)(0u);\n"
+                      << "        uint32_t x[8] = {l[" << c << "][0], l[" << c << "][1], l[" << c << "][2], l[" << c
+                      << "][3], hh[0], hh[1], hh[2], hh[3]};\n";
+                    if (p.uf_k > 0 && p.uf_inputs && row < p.uf_k)
+                        o << "        if (ufp && active) { hb_uf_put(ufp, S, " << row
+                          << "u, off, x[0], x[1], x[2], x[3]); if (full) hb_uf_put(ufp, S, " << row
+                          << "u, off2, x[4], x[5], x[6], x[7]); }\n";
+                }
+                o << "        hb_tr(x);\n"
+                     "        hb_pl[" << (jj - lo) << "][0][lane] = (u32x4){x[0], x[1], x[2], x[3]};\n"
+                     "        hb_pl[" << (jj - lo) << "][1][lane] = (u32x4){x[4], x[5], x[6], x[7]};\n"
+                     "      }\n";
+            }
+            if (!mine.empty()) o << "    }\n";
+            o << "    __syncthreads();\n";
+            // phase 2: this wave's pass over the stage's inputs
+            for (int jj = lo; jj < hi && rows; ++jj) {
+                o << "    { const u32x4 pa_ = hb_pl[" << (jj - lo) << "][0][lane], pb_ = hb_pl[" << (jj - lo)
+                  << "][1][lane];\n"
+                     "      const uint32_t x[8] = {pa_[0], pa_[1], pa_[2], pa_[3], pb_[0], pb_[1], pb_[2], pb_[3]};\n";
+                gen_network(o, cv, t0, rows, (size_t)jj, rt, p.net);
+                o << "      for (int t_ = 0; t_ < " << rows << "; ++t_) for (int q_ = 0; q_ < 8; ++q_) "
+                     "__asm__ volatile(\"\" : \"+v\"(a[t_][q_]));\n"
+                     "      __asm__ volatile(\"\" ::: \"memory\");\n    }\n";
+            }
+            if (st + 1 < nstage) o << "    __syncthreads();\n";
+        }
+        if (rows) {
+            o << "    if (active) {\n";
+            for (int t = 0; t < rows; ++t) {
+                const int row = p.out_rows[t0 + t];
+                const std::string at = "a[" + std::to_string(t) + "]";
+                o << "      { hb_tr(" << at << "); const unsigned so_ = " << rin(row) << "u * sst;\n"
+                  << "        __builtin_amdgcn_raw_buffer_store_b128((u32x4){" << at << "[0], " << at << "[1], "
+                  << at << "[2], " << at << "[3]}, rs" << blk(row) << ", off, so_, HB_ST_AUX);\n"
+                  << "        if (full) __builtin_amdgcn_raw_buffer_store_b128((u32x4){" << at << "[4], " << at
+                  << "[5], " << at << "[6], " << at << "[7]}, rs" << blk(row) << ", off2, so_, HB_ST_AUX); }\n";
+                if (p.uf_k > 0 && row < p.uf_k)
+                    o << "      if (ufp) { hb_uf_put(ufp, S, " << row << "u, off, " << at << "[0], " << at
+                      << "[1], " << at << "[2], " << at << "[3]); if (full) hb_uf_put(ufp, S, " << row
+                      << "u, off2, " << at << "[4], " << at << "[5], " << at << "[6], " << at << "[7]); }\n";
+            }
+            o << "    }\n";
+        }
+        o << "    break; }\n";
+    }
+    o << "  }\n}\n#undef HB_LD\n" << (fused ? "#undef HB_LDF\n#undef HB_LDF2\n" : "");
     return o.str();
 }
 
@@ -513,8 +688,11 @@ std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt) {
 }
 
 std::string gen_xor_source(const XorProgram &p) {
-    std::string s = std::string(kPrelude) + gen_xor_kernel(p, false);
-    if (p.fused) s += gen_xor_kernel(p, true);
+    const int npass = (int)((p.out_rows.size() + p.rt - 1) / p.rt);
+    const bool lds = p.lds && npass >= 2 && npass <= 8;
+    auto gen = [&](bool fused) { return lds ? gen_xor_kernel_lds(p, fused) : gen_xor_kernel(p, fused); };
+    std::string s = std::string(kPrelude) + gen(false);
+    if (p.fused) s += gen(true);
     return s;
 }
 

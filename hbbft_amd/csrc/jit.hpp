@@ -41,6 +41,15 @@ struct XorProgram {
     // of a pattern writes them); 0 = none
     int uf_k = 0;
     bool uf_inputs = false;
+    // LDS-staged form (gen_xor_kernel_lds): each input transposed once per
+    // workgroup, planes shared through LDS; stages of lds_stage inputs
+    bool lds = false;
+    int lds_stage = 0;
+    // network: 0 auto (nibble-subset for passes <= 8 rows, else pairwise),
+    // 1 pairwise, 2 nibble-subset
+    int net = 0;
+    // > 0: amdgpu_waves_per_eu (the register budget the compiler targets)
+    int wpe = 0;
 };
 
 // Kernel argument list shared by every generated kernel (hipModuleLaunchKernel).

@@ -125,6 +125,20 @@ class Scenario:
                                                 fake_list=fl).items()}
 
 
+def honest_tensors(n, proposers, device):
+    """Scenario tensors of honest instances: proposers [count] (a tensor or
+    list), every node honest, every Value from codeword 0, no injection."""
+    dev = torch.device("cuda", device) if isinstance(device, int) else device
+    prop = torch.as_tensor(proposers, dtype=torch.uint8).to(dev)
+    cnt = prop.shape[0]
+    W = (n + 31) // 32
+    z = torch.zeros((cnt, n), dtype=torch.uint8, device=dev)
+    return dict(proposer=prop, role=z, value_root=z, value_tamper=z,
+                fake_from=torch.full((cnt,), NONE, dtype=torch.uint8, device=dev),
+                fake_root=torch.zeros(cnt, dtype=torch.uint8, device=dev),
+                fake_list=torch.zeros((cnt, W), dtype=torch.int32, device=dev))
+
+
 def tampered(p):
     """The corrupted copy of a proof a CORRUPT_ECHO node (or a tampering
     proposer) sends: first value byte flipped, index / digests / root kept."""
@@ -173,13 +187,14 @@ def data_plane(scn, device=0):
 # ------------------------------------------------------------- one rank -----
 class StateMachineRank:
     """The hosted nodes [node_lo, node_lo + R) of rank `rank` of `world` for
-    every instance of a scenario (R = ceil(n / world))."""
+    `count` instances (R = ceil(n / world)).  `sc`: the scenario tensors
+    (Scenario.tensors or honest_tensors); ok / dec: the data plane's
+    proof_ok [count][roots][2][n] and decode_ok [count][roots]."""
 
-    def __init__(self, scn, rank, world, device=0, max_out=24, max_faults=32, ok=None,
-                 dec=None):
-        self.scn, self.rank, self.world = scn, rank, world
-        n, cnt = scn.n, scn.count
-        self.n, self.count = n, cnt
+    def __init__(self, n, count, roots, sc, rank, world, device=0, max_out=24, max_faults=32,
+                 ok=None, dec=None):
+        self.n, self.count, self.roots = n, count, roots
+        self.rank, self.world = rank, world
         self.R = -(-n // world)
         self.node_lo = rank * self.R
         self.W = (n + 31) // 32
@@ -189,9 +204,9 @@ class StateMachineRank:
         dev = self.rb.device
         self.device = dev
         L = _bind()
-        sb = L.hbrbc_sm_state_bytes(n, scn.roots)
-        R = self.R
-        self.sc = scn.tensors(dev)
+        sb = L.hbrbc_sm_state_bytes(n, roots)
+        R, cnt = self.R, count
+        self.sc = sc
         self.ok, self.dec = ok, dec
         self.state = torch.zeros((cnt, R, sb), dtype=torch.uint8, device=dev)
         self.out = torch.zeros((cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
@@ -203,12 +218,34 @@ class StateMachineRank:
         # every sender's records of the previous round, [G][count][R][E][rec]
         self.inbox = torch.zeros((world, cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
         self.inbox_count = torch.zeros((world, cnt, R), dtype=torch.int32, device=dev)
+        self.records = 0   # records emitted over the last run (all rounds)
+
+    @classmethod
+    def from_scenario(cls, scn, rank, world, device=0, max_out=24, max_faults=32, ok=None,
+                      dec=None):
+        dev = torch.device("cuda", device) if isinstance(device, int) else device
+        return cls(scn.n, scn.count, scn.roots, scn.tensors(dev), rank, world, device, max_out,
+                   max_faults, ok, dec)
+
+    def reset(self):
+        """Fresh nodes (before round 0 of another run)."""
+        self.state.zero_()
+        self.out_count.zero_()
+        self.inbox_count.zero_()
+        self.output_root.fill_(NONE)
+        self.fault_count.zero_()
+        self.records = 0
+
+    def swap_local(self):
+        """One rank: this round's records become the next round's inbox."""
+        self.inbox, self.out = self.out.unsqueeze(0), self.inbox[0]
+        self.inbox_count, self.out_count = self.out_count.unsqueeze(0), self.inbox_count[0]
 
     def round(self, r, stream=None):
         """Handle round r's inbox (round 0: the proposers' broadcast())."""
         s = self.sc
         a = SmArgs(count=self.count, node_lo=self.node_lo, nodes=self.R, rows_per_rank=self.R,
-                   roots=self.scn.roots, max_out=self.max_out, max_faults=self.max_faults, round=r)
+                   roots=self.roots, max_out=self.max_out, max_faults=self.max_faults, round=r)
         for name in ("proposer", "role", "value_root", "value_tamper", "fake_from", "fake_root",
                      "fake_list"):
             setattr(a, name, s[name].data_ptr())
@@ -270,19 +307,28 @@ class LoopbackExchange:
             r.inbox_count.copy_(cnts)
 
 
-def run_rounds(ranks, exchange=None, max_rounds=64):
+def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
     """Drive the state machine until no node emits a message.  `ranks`: the
-    StateMachineRank objects of this process (all of them for a loopback
-    run, one with a DistExchange `exchange`).  Returns the number of rounds."""
+    StateMachineRank objects of this process -- all virtual ranks of one
+    topology for a loopback run (exchange None), or independent objects of
+    this rank (e.g. pipelined sub-batches) with a DistExchange / SoloExchange
+    `exchange`, whose world they share.  Returns the number of rounds."""
     import torch.distributed as dist
-    loop = LoopbackExchange(ranks) if exchange is None else None
+    if fresh:
+        for sm in ranks:
+            sm.reset()
+    loop = LoopbackExchange(ranks) if exchange is None and len(ranks) > 1 else None
+    world = exchange.world if exchange is not None else 1
     for r in range(max_rounds):
         for sm in ranks:
             sm.round(r)
         for sm in ranks:
             sm.check_overflow()
-        emitted = sum(int(sm.emitted.item()) for sm in ranks)
-        if exchange is not None and exchange.world > 1:
+        counts = [int(sm.emitted.item()) for sm in ranks]
+        for sm, c in zip(ranks, counts):
+            sm.records += c
+        emitted = sum(counts)
+        if world > 1:
             t = torch.tensor([emitted], dtype=torch.int64, device=ranks[0].device)
             if exchange.staged:
                 t = t.cpu()
@@ -292,10 +338,16 @@ def run_rounds(ranks, exchange=None, max_rounds=64):
             return r + 1
         if loop is not None:
             loop.gather()
-        else:
-            for h in ranks[0].exchange(exchange):
+        elif world > 1:
+            hs = []
+            for sm in ranks:
+                hs += sm.exchange(exchange)
+            for h in hs:
                 if h is not None:
                     h.wait()
+        else:
+            for sm in ranks:
+                sm.swap_local()
     raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
 
 
@@ -304,7 +356,7 @@ def simulate(scn, world=1, device=0, max_out=24, max_faults=32):
     GPU.  Returns ({(inst, node): output bytes or None}, {(inst, node): fault
     list}, rounds)."""
     ok, dec, payloads, _ = data_plane(scn, device)
-    ranks = [StateMachineRank(scn, g, world, device, max_out, max_faults, ok, dec)
+    ranks = [StateMachineRank.from_scenario(scn, g, world, device, max_out, max_faults, ok, dec)
              for g in range(world)]
     rounds = run_rounds(ranks)
     outputs, faults = {}, {}

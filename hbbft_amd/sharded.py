@@ -301,6 +301,19 @@ class ShardedBroadcast:
         self.echo_senders = torch.zeros(G * C, dtype=torch.int32, device=dev)
         self.full_echos = torch.zeros(G * C, dtype=torch.int32, device=dev)
         self.decided = torch.zeros(G * C, dtype=torch.bool, device=dev)
+        # the Broadcast state machine of every hosted validator for every
+        # instance (hbbft_amd/rbc_sim.py, sim.hip): Echo / EchoHash / Ready /
+        # CanDecode handling with per-node counters, fed by this step's
+        # validations and decodes; instance (s, i) = s * C + i, proposed by
+        # validator proposers(s, C)[i]
+        from .rbc_sim import StateMachineRank, honest_tensors
+        props = [p_ for s_ in range(G) for p_ in t.proposers(s_, C)]
+        self.sm_ok = torch.zeros((G * C, 1, 2, n), dtype=torch.uint8, device=dev)
+        self.sm_dec = torch.zeros((G * C, 1), dtype=torch.uint8, device=dev)
+        self.sm = StateMachineRank(n, G * C, 1, honest_tensors(n, props, dev), rank, world,
+                                   device=device, max_out=4, max_faults=4, ok=self.sm_ok,
+                                   dec=self.sm_dec)
+        self.sm_rounds = 0
         self.own_cols = torch.tensor([j - rank * R for j in own] or [0], dtype=torch.int64,
                                      device=dev)
         self.own_rows = torch.tensor(own or [0], dtype=torch.int64, device=dev)
@@ -411,20 +424,30 @@ class ShardedBroadcast:
         self.thresholds()
 
     def thresholds(self):
-        """The state machine's counters for receiver r0, per instance, on the
-        device.  A validator whose Value validated sends Echo to its left nodes
-        and EchoHash to its right ones, and count_echos counts both
-        (broadcast.rs:413-425, 456-468), so Ready goes out once N-f validators
-        validated their Values (310-312, and on f+1 Readys everyone follows,
-        396-402); compute_output then needs > 2f Readys and >= k full Echoes at
-        r0 (526-532).  decided[i]: the receivers output instance i (status
-        tells with what); otherwise no node decides it."""
+        """Inputs of the state machine from this step's data plane: proof (0,
+        j) of every instance validates iff validator j's Value did (the Echo
+        it forwards is the same proof, broadcast.rs:254, 291), and root 0
+        decodes iff this rank's decode of the instance succeeded (a codeword
+        decodes from any k of its rows, 551-557); plus the data-plane counts
+        echo_senders (validators whose Value validated, i.e. that send Echo /
+        EchoHash, 413-425, 456-468) and full_echos (Echoes receiver r0 holds)."""
         t, G, C = self.topo, self.world, self.count
         valid = self.okv_all.transpose(0, 1).reshape(G * C, t.npad)[:, : t.n]
         torch.sum(valid, dim=1, dtype=torch.int32, out=self.echo_senders)
         torch.sum(self.present, dim=1, dtype=torch.int32, out=self.full_echos)
-        readys = torch.where(self.echo_senders >= t.n - t.f, t.n, 0)
-        torch.logical_and(readys > 2 * t.f, self.full_echos >= self.rb.k, out=self.decided)
+        self.sm_ok[:, 0, 0, :].copy_(valid)
+        self.sm_dec[:, 0].copy_(self.status == 0)
+
+    def finish(self):
+        """After the state machine's rounds: decided[i] = every validator this
+        rank hosts output instance i (compute_output, broadcast.rs:526-558:
+        > 2f Readys and >= k full Echoes, Ready sent at N - f Echoes or f + 1
+        Readys)."""
+        out = self.sm.output_root[:, : self.vreal]
+        torch.all(out == 0, dim=1, out=self.decided)
+
+    def state_machine(self, ex):
+        self.sm_rounds = run_state_machines([self], ex)
 
     def step(self, payloads, ex):
         self.propose(payloads)
@@ -434,6 +457,7 @@ class ShardedBroadcast:
         self.exchange_echo(ex)
         self.validate_echoes()
         self.decode()
+        self.state_machine(ex)
 
     # accounting --------------------------------------------------------------
     def counts(self):
@@ -450,6 +474,9 @@ class ShardedBroadcast:
             "faithful_echo_validates": inst * self.vreal * (t.n - t.f),
             "faithful_decodes": inst * self.vreal,
             "faithful_decode_leaf_hashes": inst * self.vreal * t.n,
+            "state_machine_nodes": inst * self.vreal,
+            "state_machine_rounds": self.sm_rounds,
+            "state_machine_messages": self.sm.records,
         }
 
 
@@ -474,3 +501,21 @@ def pipelined_step(subs, payloads, ex, timer):
         cur.wait_event(ev_e[i])
         sb.validate_echoes()
         sb.decode()
+    # every sub-batch's state machine in lockstep: one exchange per round
+    rounds = run_state_machines(subs, ex)
+    for sb in subs:
+        sb.sm_rounds = rounds
+
+
+def run_state_machines(subs, ex):
+    """Rounds of the Broadcast state machine (rbc_sim.run_rounds) of several
+    ShardedBroadcast objects of this rank, their messages all-gathered over
+    `ex` each round; then every object's decided flags."""
+    from .rbc_sim import run_rounds
+    if ex.world > 1:
+        rounds = run_rounds([sb.sm for sb in subs], ex)
+    else:   # one rank: each object's nodes only talk to themselves
+        rounds = max(run_rounds([sb.sm]) for sb in subs)
+    for sb in subs:
+        sb.finish()
+    return rounds

@@ -167,6 +167,13 @@ def run_loopback(n, world, count, plen, tamper=None, specialise=True):
     for sb in ranks:
         sb.validate_echoes()
         sb.decode()
+    # the state machine of every validator, the virtual ranks' messages
+    # all-gathered (loopback) each round
+    from hbbft_amd.rbc_sim import run_rounds
+    rounds = run_rounds([sb.sm for sb in ranks])
+    for sb in ranks:
+        sb.finish()
+        sb.sm_rounds = rounds
     torch.cuda.synchronize()
     return ranks, pays
 
