@@ -539,7 +539,9 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
         for key, v in s_.counts().items():
-            counts[key] = counts.get(key, 0) + v
+            # sub-batches run their state machines in lockstep: rounds are shared
+            counts[key] = max(counts.get(key, 0), v) if key == "state_machine_rounds" \
+                else counts.get(key, 0) + v
     t = sb.topo
     # bytes each rank moves per step: Value all-to-all sends (G-1)/G of its
     # slab + digests; the Echo all-gather brings in the other ranks' rows of

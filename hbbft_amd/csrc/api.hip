@@ -267,6 +267,11 @@ struct hbrbc_ctx {
         std::vector<uint8_t> present;
     };
     std::map<int, DecSpec> dec_spec;
+    std::string jit_missing;   // HBRBC_JIT=load: why an encoder code object is missing
+    // side streams + events for the concurrent launch of a matrix's programs
+    // (HBRBC_XOR_STREAMS, launch_groups)
+    std::vector<hipStream_t> side;
+    std::vector<hipEvent_t> side_ev;
     DevBuf d_matrix, d_enc_coefs, d_enc_in, d_enc_out;
     // reconstruct workspace: decode-matrix cache + per-call scratch
     size_t ws_count = 0;
@@ -468,6 +473,8 @@ int run_merkle(hbrbc_ctx *c, const uint8_t *shards, size_t shard_len, const RowM
 
 hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, XorArgs a,
                             size_t count, hipStream_t s);
+hipError_t launch_groups(hbrbc_ctx *c, const std::vector<hbrbc_ctx::SpecGroup> &gs, size_t first,
+                         int rt, const XorArgs &x, size_t count, hipStream_t s);
 
 // Fused unframe (decode paths): the generic reconstruct kernel writes the
 // payload bytes of the data rows it reads or rebuilds, so unframe's re-read of
@@ -482,6 +489,20 @@ bool unframe_fusable(const hbrbc_ctx *c, size_t shard_len, size_t payload_stride
            (uint64_t)c->k * shard_len > 4;
 }
 
+// HBRBC_JIT: unset = encoders from the code-object cache when present,
+// decoders compiled on a miss; "0" = no specialised encoders; "1" = compile
+// any missing code object; "load" = cache only, and a missing code object is
+// an error (proves build() pre-built every object a run needs).
+enum JitMode { JIT_DEFAULT, JIT_OFF, JIT_COMPILE, JIT_LOAD };
+JitMode jit_mode() {
+    const char *e = getenv("HBRBC_JIT");
+    if (!e) return JIT_DEFAULT;
+    if (!std::strcmp(e, "0")) return JIT_OFF;
+    if (!std::strcmp(e, "1")) return JIT_COMPILE;
+    if (!std::strcmp(e, "load")) return JIT_LOAD;
+    return JIT_DEFAULT;
+}
+
 bool decode_programs(const std::vector<uint8_t> &mat, size_t k, size_t n, const uint8_t *present,
                      int rb, std::vector<XorProgram> &out, uint64_t &hash, int &rt, bool uf);
 int load_program(const XorProgram &p, bool compile, hbrbc_ctx::SpecGroup &g);
@@ -494,8 +515,7 @@ bool uf_decoder(hbrbc_ctx *c, hbrbc_ctx::DecSpec &d, int rb) {
         std::vector<XorProgram> progs;
         uint64_t hash = 0;
         int rt = 2;
-        const char *mode = getenv("HBRBC_JIT");
-        const bool compile = !(mode && !std::strcmp(mode, "0"));
+        const bool compile = jit_mode() == JIT_DEFAULT || jit_mode() == JIT_COMPILE;
         const std::string saved = g_err;
         d.uf_state = -1;
         if (decode_programs(c->matrix, c->k, c->n, d.present.data(), rb, progs, hash, rt, true)) {
@@ -573,8 +593,8 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
             x.uf_stride = uf_stride;
             x.uf_status = status;
         }
-        for (const auto &g : uf_payload ? ds->second.uf_groups : ds->second.groups)
-            HB_HIP(launch_xor_group(g, false, ds->second.rt, x, count, s));
+        HB_HIP(launch_groups(c, uf_payload ? ds->second.uf_groups : ds->second.groups, 0,
+                             ds->second.rt, x, count, s));
     }
     GfApplyArgs g{};
     g.base = shards;
@@ -837,10 +857,9 @@ const std::vector<hbrbc_ctx::SpecGroup> *spec_encoder(hbrbc_ctx *c, int rb) {
     auto it = c->enc_spec.find(rb);
     if (it != c->enc_spec.end()) return it->second.empty() ? nullptr : &it->second;
     std::vector<hbrbc_ctx::SpecGroup> gs;
-    const char *mode = getenv("HBRBC_JIT");
-    const bool off = c->m == 0 || (mode && !std::strcmp(mode, "0")) || c->k * c->m > 16384;
+    const bool off = c->m == 0 || jit_mode() == JIT_OFF || c->k * c->m > 16384;
     if (!off) {
-        const bool compile = mode && !std::strcmp(mode, "1");
+        const bool compile = jit_mode() == JIT_COMPILE;
         const std::string saved = g_err;
         for (const auto &rg : xor_groups(c->k, c->m, c->rt_spec)) {
             const XorProgram p = encode_program(c->k, c->m, c->matrix.data() + c->k * c->k,
@@ -852,7 +871,12 @@ const std::vector<hbrbc_ctx::SpecGroup> *spec_encoder(hbrbc_ctx *c, int rb) {
             }
             gs.push_back(g);
         }
-        g_err = saved;  // a missing code object is not an error of the caller's call
+        if (gs.empty() && jit_mode() == JIT_LOAD) {
+            // keep the load error: the caller fails instead of falling back
+            c->jit_missing = g_err;
+        } else {
+            g_err = saved;  // a missing code object is not an error of the caller's call
+        }
     }
     auto &slot = c->enc_spec[rb];
     slot = std::move(gs);
@@ -891,6 +915,51 @@ hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, X
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// The programs of a matrix split over several code objects (N = 250: four
+// groups of output rows) read the same input rows.  Launched one after the
+// other, each streams every instance's inputs from HBM again (cfg5: 1.95x /
+// 2.29x the algorithmic bytes, profiles/pmc_traffic.json); launched
+// concurrently on side streams they walk the instances together, so each
+// input row is fetched once and served to the other programs from L2 /
+// MALL.  HBRBC_XOR_STREAMS=0 keeps the serial order (A/B).
+bool xor_streams() {
+    const char *e = getenv("HBRBC_XOR_STREAMS");
+    return !(e && !std::strcmp(e, "0"));
+}
+
+hipError_t launch_groups(hbrbc_ctx *c, const std::vector<hbrbc_ctx::SpecGroup> &gs, size_t first,
+                         int rt, const XorArgs &x, size_t count, hipStream_t s) {
+    const size_t ng = gs.size() - first;
+    if (ng == 0) return hipSuccess;
+    if (ng == 1 || !xor_streams()) {
+        for (size_t i = first; i < gs.size(); ++i) {
+            const hipError_t e = launch_xor_group(gs[i], false, rt, x, count, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    while (c->side.size() < ng) {
+        hipStream_t q;
+        hipError_t e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+        c->side.push_back(q);
+    }
+    while (c->side_ev.size() < ng + 1) {
+        hipEvent_t ev;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        c->side_ev.push_back(ev);
+    }
+    hipError_t e = hipEventRecord(c->side_ev[ng], s);   // inputs ready on s
+    for (size_t i = 0; i < ng && e == hipSuccess; ++i) {
+        e = hipStreamWaitEvent(c->side[i], c->side_ev[ng], 0);
+        if (e == hipSuccess) e = launch_xor_group(gs[first + i], false, rt, x, count, c->side[i]);
+        if (e == hipSuccess) e = hipEventRecord(c->side_ev[i], c->side[i]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, c->side_ev[i], 0);
+    }
+    return e;
 }
 
 std::once_flag g_default_once;
@@ -941,9 +1010,11 @@ int encode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &r
         x.block_stride = rows.bst;
         x.row_bytes = (unsigned)round_up(shard_len, 16);
         x.p_only = -1;
-        for (const auto &grp : *gs) HB_HIP(launch_xor_group(grp, false, c->rt_spec, x, count, s));
+        HB_HIP(launch_groups(c, *gs, 0, c->rt_spec, x, count, s));
         return HBRBC_OK;
     }
+    if (jit_mode() == JIT_LOAD && c->k * c->m <= 16384)
+        return fail(HBRBC_E_INVALID_ARG, "HBRBC_JIT=load: %s", c->jit_missing.c_str());
     return generic_encode(c, shards, shard_len, rows, inst_stride, count, s);
 }
 
@@ -1094,8 +1165,12 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
     c->depth_spec = spec_depth();
     c->enc_kind = c->m == 0 ? "trivial" : (spec_encoder(c, 256) ? "specialised" : "bitslice");
     if (c->m > 0 && c->enc_kind == "bitslice") {
-        const char *mode = getenv("HBRBC_JIT");
-        if (mode && !std::strcmp(mode, "1") && c->k * c->m <= 16384) c->enc_kind = "jit-failed";
+        if (jit_mode() == JIT_COMPILE && c->k * c->m <= 16384) c->enc_kind = "jit-failed";
+        if (jit_mode() == JIT_LOAD && c->k * c->m <= 16384) {
+            const std::string msg = c->jit_missing;
+            hbrbc_coding_free(c);
+            return fail(HBRBC_E_INVALID_ARG, "HBRBC_JIT=load: %s", msg.c_str());
+        }
     }
     *out = c;
     return HBRBC_OK;
@@ -1112,6 +1187,8 @@ void hbrbc_coding_free(hbrbc_ctx *c) {
         b->release();
     c->pin.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->side_ev) (void)hipEventDestroy(e);
+    for (hipStream_t q : c->side) (void)hipStreamDestroy(q);
     for (auto &kv : c->enc_spec) drop_groups(kv.second);
     for (auto &kv : c->dec_spec) {
         drop_groups(kv.second.groups);
@@ -1199,6 +1276,8 @@ int hbrbc_frame_encode_rows(hbrbc_ctx *c, const uint8_t *payloads, size_t payloa
     if (c->m > 0 && shard_stride == round_up(shard_len, 16) && payload_len <= 0x7FFFFFFFull &&
         shard_len * c->k < 0x7FFFFFFFull)
         gs = spec_encoder(c, code_rb(rows));
+    if (!gs && jit_mode() == JIT_LOAD && c->m > 0 && c->k * c->m <= 16384)
+        return fail(HBRBC_E_INVALID_ARG, "HBRBC_JIT=load: %s", c->jit_missing.c_str());
     const char *fe = getenv("HBRBC_FUSE");   // 0: frame kernel + encoder (A/B)
     if (!gs || (fe && !std::strcmp(fe, "0"))) {
         st = frame_rows(c, payloads, payload_stride, payload_len, count, shards, shard_len, rows,
@@ -1227,8 +1306,7 @@ int hbrbc_frame_encode_rows(hbrbc_ctx *c, const uint8_t *payloads, size_t payloa
     HB_HIP(launch_frame_fixup(payloads, payload_stride, payload_len, shards, shard_len, rows,
                               inst_stride, c->k, (size_t)g0.r_hi, c->d_matrix.as<uint8_t>(), count,
                               s));
-    for (size_t i = 1; i < gs->size(); ++i)
-        HB_HIP(launch_xor_group((*gs)[i], false, c->rt_spec, x, count, s));
+    HB_HIP(launch_groups(c, *gs, 1, c->rt_spec, x, count, s));
     return HBRBC_OK;
 }
 
@@ -1505,8 +1583,7 @@ int hbrbc_decoder_specialise(hbrbc_ctx *c, const uint8_t *present, size_t rows_p
     int rt = 2;
     if (!decode_programs(c->matrix, c->k, c->n, present, rb, progs, hash, rt))
         return fail(HBRBC_E_INVALID_ARG, "pattern has nothing to rebuild or too few shards");
-    const char *mode = getenv("HBRBC_JIT");
-    const bool compile = !(mode && !std::strcmp(mode, "0"));
+    const bool compile = jit_mode() == JIT_DEFAULT || jit_mode() == JIT_COMPILE;
     hbrbc_ctx::DecSpec d;
     d.hash = hash;
     d.rt = rt;

@@ -267,6 +267,151 @@ __device__ __forceinline__ void sha3_256_pair(const uint32_t (&a)[8], const uint
     }
 }
 
+// ------------------------------------------------ pair-lane Keccak (A/B) --
+// One sponge on TWO lanes (north_star "wave-per-leaf" direction, VERDICT r2
+// item 6): lane parity h = lane & 1 holds half h of every 64-bit state word
+// (h = 0 the low 32 bits).  A 64-bit rotation then needs the partner's half:
+// one DPP swap of adjacent lanes (quad_perm [1,0,3,2]) plus one
+// v_alignbit per word, the same expression on both lanes:
+//   rotl64(w, r) half h = alignbit(mine, partner, 32 - r)      r < 32
+//                       = alignbit(partner, mine, 64 - r)      r > 32
+// Per lane and round: theta 10 + 25 xor3, 5 + 24 DPP moves, 5 + 24 alignbit,
+// chi 25 bitop3, iota 2: ~120 VALU per lane, ~240 per sponge (180 on one
+// lane) -- twice the lanes per sponge for grids too small to fill the chip
+// and for the latency of a lone sponge (per-call Proof::validate).
+__device__ __forceinline__ uint32_t pl_partner(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // lanes 1,0,3,2
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t pl_rot(uint32_t mine) {
+    if constexpr (R == 0) {
+        return mine;
+    } else {
+        const uint32_t other = pl_partner(mine);
+        if constexpr (R == 32) return other;
+        else if constexpr (R < 32) return __builtin_amdgcn_alignbit(mine, other, 32 - R);
+        else return __builtin_amdgcn_alignbit(other, mine, 64 - R);
+    }
+}
+
+#define HB_PL_RHOPI(src, dst, r) B[dst] = pl_rot<r>(S[src])
+__device__ __forceinline__ void keccak_f1600_pl(uint32_t (&S)[25], uint32_t h) {
+#pragma unroll HB_KECCAK_UNROLL
+    for (int round = 0; round < 24; ++round) {
+        uint32_t C[5], D[5];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) C[x] = xor3(xor3(S[x], S[x + 5], S[x + 10]), S[x + 15], S[x + 20]);
+#pragma unroll
+        for (int x = 0; x < 5; ++x) D[x] = pl_rot<1>(C[(x + 1) % 5]);
+#pragma unroll
+        for (int i = 0; i < 25; ++i) S[i] = xor3(S[i], C[(i + 4) % 5], D[i % 5]);
+        uint32_t B[25];
+        HB_PL_RHOPI(0, 0, 0);
+        HB_PL_RHOPI(5, 16, 36);
+        HB_PL_RHOPI(10, 7, 3);
+        HB_PL_RHOPI(15, 23, 41);
+        HB_PL_RHOPI(20, 14, 18);
+        HB_PL_RHOPI(1, 10, 1);
+        HB_PL_RHOPI(6, 1, 44);
+        HB_PL_RHOPI(11, 17, 10);
+        HB_PL_RHOPI(16, 8, 45);
+        HB_PL_RHOPI(21, 24, 2);
+        HB_PL_RHOPI(2, 20, 62);
+        HB_PL_RHOPI(7, 11, 6);
+        HB_PL_RHOPI(12, 2, 43);
+        HB_PL_RHOPI(17, 18, 15);
+        HB_PL_RHOPI(22, 9, 61);
+        HB_PL_RHOPI(3, 5, 28);
+        HB_PL_RHOPI(8, 21, 55);
+        HB_PL_RHOPI(13, 12, 25);
+        HB_PL_RHOPI(18, 3, 21);
+        HB_PL_RHOPI(23, 19, 56);
+        HB_PL_RHOPI(4, 15, 27);
+        HB_PL_RHOPI(9, 6, 20);
+        HB_PL_RHOPI(14, 22, 39);
+        HB_PL_RHOPI(19, 13, 8);
+        HB_PL_RHOPI(24, 4, 14);
+#pragma unroll
+        for (int y = 0; y < 25; y += 5)
+#pragma unroll
+            for (int x = 0; x < 5; ++x) S[y + x] = B[y + x] ^ (~B[y + (x + 1) % 5] & B[y + (x + 2) % 5]);
+        S[0] ^= h ? kRcHi[round] : kRcLo[round];
+    }
+}
+#undef HB_PL_RHOPI
+
+// SHA3-256 of `len` bytes at `p` on a lane pair: this lane absorbs half h of
+// every 8-byte word (the dword at 8w + 4h); the digest comes out whole on
+// both lanes.  Both lanes of a pair take every branch together.
+__device__ __forceinline__ void sha3_256_row_pl(const uint8_t *__restrict__ p, uint32_t len,
+                                                uint32_t h, uint32_t (&out)[8]) {
+    uint32_t S[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) S[i] = 0u;
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p) + h;
+    const uint32_t nfull = len / 136u;
+    if (nfull) {
+        uint32_t nx[17];
+#pragma unroll
+        for (int w = 0; w < 17; ++w) nx[w] = q[2 * w];
+        for (uint32_t t = 0; t < nfull; ++t) {
+#pragma unroll
+            for (int w = 0; w < 17; ++w) S[w] ^= nx[w];
+            q += 34;
+            if (t + 1 < nfull) {
+#pragma unroll
+                for (int w = 0; w < 17; ++w) nx[w] = q[2 * w];
+            }
+            keccak_f1600_pl(S, h);
+        }
+    }
+    const int r = (int)(len - nfull * 136u);
+    const uint8_t *tail = reinterpret_cast<const uint8_t *>(q - h);
+#pragma unroll
+    for (int w = 0; w < 17; ++w) {
+        const int rem = r - 8 * w;   // bytes of this 8-byte word still in the message
+        const int mine = rem - 4 * (int)h;   // ... in this lane's half
+        uint32_t v = 0;
+        if (mine > 0) {
+            v = reinterpret_cast<const uint32_t *>(tail)[2 * w + h];
+            if (mine < 4) v &= 0xFFFFFFFFu >> (8 * (4 - mine));
+        }
+        if (mine >= 0 && mine < 4) v ^= 0x06u << (8 * mine);   // domain byte
+        S[w] ^= v;
+    }
+    if (h) S[16] ^= 0x80000000u;
+    keccak_f1600_pl(S, h);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t other = pl_partner(S[w]);
+        out[2 * w] = h ? other : S[w];
+        out[2 * w + 1] = h ? S[w] : other;
+    }
+}
+
+// SHA3-256(a ++ b) of two digests on a lane pair (hash_pair, merkle.rs:137-140).
+__device__ __forceinline__ void sha3_256_pair_pl(const uint32_t (&a)[8], const uint32_t (&b)[8],
+                                                 uint32_t h, uint32_t (&out)[8]) {
+    uint32_t S[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) S[i] = 0u;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        S[w] = h ? a[2 * w + 1] : a[2 * w];
+        S[w + 4] = h ? b[2 * w + 1] : b[2 * w];
+    }
+    S[8] = h ? 0u : 0x06u;
+    S[16] = h ? 0x80000000u : 0u;
+    keccak_f1600_pl(S, h);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t other = pl_partner(S[w]);
+        out[2 * w] = h ? other : S[w];
+        out[2 * w + 1] = h ? S[w] : other;
+    }
+}
+
 __device__ __forceinline__ void load_digest(const uint8_t *p, uint32_t (&d)[8]) {
     const uint4 *q = reinterpret_cast<const uint4 *>(p);
     uint4 a = q[0], b = q[1];

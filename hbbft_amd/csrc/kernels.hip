@@ -636,6 +636,73 @@ __global__ HB_SPONGE_ATTR void validate_kernel(
     ok_out[g] = ok ? 1 : 0;
 }
 
+// Pair-lane forms (device_common.hpp keccak_f1600_pl): one sponge on two
+// lanes, for grids too small to fill the chip and for the per-call shims
+// (HBRBC_SPONGE_PAIR, launch_leaf_hash / launch_validate).
+__global__ __launch_bounds__(kBlock) void leaf_hash_pl_kernel(
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
+    uint32_t n, size_t total, uint8_t *__restrict__ nodes, size_t node_inst_stride,
+    const uint32_t *__restrict__ slens) {
+    const size_t g = (blockIdx.x * (size_t)kBlock + threadIdx.x) >> 1;
+    const uint32_t h = threadIdx.x & 1u;
+    if (g >= total) return;   // both lanes of a pair leave together
+    const size_t inst = g / n;
+    const uint32_t i = (uint32_t)(g - inst * n);
+    if (slens) S = min(slens[inst], (uint32_t)rows.sst);
+    uint32_t d[8];
+    sha3_256_row_pl(shards + inst * inst_stride + rows.off(i), S, h, d);
+    if (!h) store_digest(nodes + inst * node_inst_stride + (size_t)i * 32, d);
+}
+
+__global__ __launch_bounds__(kBlock) void validate_pl_kernel(
+    const uint8_t *__restrict__ values, uint32_t value_len, size_t value_inst_stride,
+    RowMap vrows, uint32_t per_inst, const uint32_t *__restrict__ rows,
+    const uint32_t *__restrict__ indices, const uint8_t *__restrict__ digests, uint32_t dslots,
+    uint32_t dig_rows, const uint8_t *__restrict__ ndig, const uint8_t *__restrict__ roots,
+    size_t root_stride, uint32_t tree_n, size_t count, uint8_t *__restrict__ ok_out,
+    uint8_t *__restrict__ leaf_out, size_t leaf_inst_stride) {
+    const size_t g = (blockIdx.x * (size_t)kBlock + threadIdx.x) >> 1;
+    const uint32_t h = threadIdx.x & 1u;
+    if (g >= count * per_inst) return;
+    const size_t inst = g / per_inst;
+    const uint32_t jj = (uint32_t)(g - inst * per_inst);
+    const uint32_t r = rows ? rows[jj] : jj;
+    uint32_t d[8];
+    sha3_256_row_pl(values + inst * value_inst_stride + vrows.off(r), value_len, h, d);
+    if (leaf_out && !h) store_digest(leaf_out + inst * leaf_inst_stride + (size_t)r * 32, d);
+    uint32_t i = indices ? indices[g] : r;
+    uint32_t lvl_n = tree_n, used = 0;
+    const size_t ps = inst * dig_rows + (rows ? r : jj);
+    const uint32_t nd = ndig[ps];
+    const uint8_t *dig = digests + ps * dslots * 32;
+    bool ok = true;
+    while (lvl_n > 1) {
+        if ((i ^ 1u) < lvl_n) {
+            if (used >= nd) {
+                ok = false;
+                break;
+            }
+            uint32_t sd[8], t[8];
+            load_digest(dig + (size_t)used * 32, sd);
+            ++used;
+            if (i & 1u)
+                sha3_256_pair_pl(sd, d, h, t);
+            else
+                sha3_256_pair_pl(d, sd, h, t);
+#pragma unroll
+            for (int w = 0; w < 8; ++w) d[w] = t[w];
+        }
+        i >>= 1;
+        lvl_n = (lvl_n + 1) >> 1;
+    }
+    if (used != nd) ok = false;
+    uint32_t rt[8];
+    load_digest(roots + inst * root_stride, rt);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) ok = ok && (rt[w] == d[w]);
+    if (!h) ok_out[g] = ok ? 1 : 0;
+}
+
 // --------------------------------------------------- decode-matrix cache --
 // Present mask of instance `inst` as 8 words (bit b of word w = present[32w+b]).
 __device__ __forceinline__ uint32_t mask_word(const uint8_t *pres, int n, int w) {
@@ -1003,6 +1070,19 @@ size_t shaped_lds(size_t lanes, int max_w, size_t static_lds = 0) {
 constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kernels (<= 128 VGPRs)
 // Grids below 2^18 sponges (< 4 waves per SIMD) take the 16-byte-load variant.
 bool few_sponges(size_t lanes) { return lanes < ((size_t)1 << 18); }
+// Pair-lane sponges (two lanes each): HBRBC_SPONGE_PAIR=1 always, =2 for
+// grids below `pair_below` sponges, 0 never (default; A/B).
+bool pair_sponges(size_t sponges) {
+    static const int mode = [] {
+        const char *e = getenv("HBRBC_SPONGE_PAIR");
+        return e ? atoi(e) : 0;
+    }();
+    static const size_t below = [] {
+        const char *e = getenv("HBRBC_SPONGE_PAIR_BELOW");
+        return e ? (size_t)atoll(e) : ((size_t)1 << 17);
+    }();
+    return mode == 1 || (mode == 2 && sponges < below);
+}
 }  // namespace
 
 void pattern_mask(const uint8_t *present, int n, uint32_t (&w)[8]) {
@@ -1127,6 +1207,12 @@ hipError_t launch_leaf_hash(const uint8_t *shards, size_t shard_len, const RowMa
                             size_t node_inst_stride, hipStream_t s, const uint32_t *slens) {
     const size_t total = n * count;
     if (total == 0) return hipSuccess;
+    if (pair_sponges(total)) {
+        hipLaunchKernelGGL(leaf_hash_pl_kernel, dim3(grid_for(2 * total, (size_t)1 << 30)),
+                           dim3(kBlock), 0, s, shards, (uint32_t)shard_len, rows, inst_stride,
+                           (uint32_t)n, total, nodes, node_inst_stride, slens);
+        return hipGetLastError();
+    }
     const bool v16 = few_sponges(total);
     hipLaunchKernelGGL(v16 ? leaf_hash_kernel<true> : leaf_hash_kernel<false>,
                        dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
@@ -1219,6 +1305,15 @@ hipError_t launch_proofs(const uint8_t *nodes, size_t node_inst_stride, size_t n
 hipError_t launch_validate(const ValidateArgs &a, hipStream_t s) {
     const size_t total = a.count * a.per_inst;
     if (total == 0) return hipSuccess;
+    if (pair_sponges(total)) {
+        hipLaunchKernelGGL(validate_pl_kernel, dim3(grid_for(2 * total, (size_t)1 << 30)),
+                           dim3(kBlock), 0, s, a.values, (uint32_t)a.value_len,
+                           a.value_inst_stride, a.vrows, (uint32_t)a.per_inst, a.rows, a.indices,
+                           a.digests, (uint32_t)a.dslots, (uint32_t)a.dig_rows, a.ndig, a.roots,
+                           a.root_stride, (uint32_t)a.tree_n, a.count, a.ok_out, a.leaf_out,
+                           a.leaf_inst_stride);
+        return hipGetLastError();
+    }
     const bool v16 = few_sponges(total);
     hipLaunchKernelGGL(v16 ? validate_kernel<true> : validate_kernel<false>,
                        dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),

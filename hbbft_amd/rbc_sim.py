@@ -351,10 +351,12 @@ def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
     raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
 
 
-def simulate(scn, world=1, device=0, max_out=24, max_faults=32):
+def simulate(scn, world=1, device=0, max_out=24, max_faults=None):
     """Every node of every instance of `scn` over `world` virtual ranks on one
     GPU.  Returns ({(inst, node): output bytes or None}, {(inst, node): fault
     list}, rounds)."""
+    if max_faults is None:   # the ProposeAdversary costs a node ~2 faults per faulty node
+        max_faults = max(32, 4 * scn.n)
     ok, dec, payloads, _ = data_plane(scn, device)
     ranks = [StateMachineRank.from_scenario(scn, g, world, device, max_out, max_faults, ok, dec)
              for g in range(world)]
