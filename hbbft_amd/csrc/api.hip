@@ -686,10 +686,12 @@ int spec_sync() {
 }
 
 // LDS-staged specialised kernels (jit.hip gen_xor_kernel_lds): every input
-// transposed once per workgroup.  HBRBC_JIT_LDS=0/1 overrides (A/B).
-bool spec_lds() {
-    const char *e = getenv("HBRBC_JIT_LDS");
-    return e && !std::strcmp(e, "1");
+// framed and transposed once per workgroup.  Default for 16..32 input rows
+// (cfg3, k = 22: frame+encode 4.25 -> 3.70 ms on one box, r3 A/B in
+// profiles/r3_enc_variants.txt); HBRBC_JIT_LDS=0/1 overrides (A/B).
+bool spec_lds(size_t nin, size_t nout) {
+    if (const char *e = getenv("HBRBC_JIT_LDS")) return !std::strcmp(e, "1");
+    return nin >= 16 && nin <= 32 && nout >= 14;
 }
 
 // XOR-network form: 0 auto, 1 pairwise, 2 nibble-subset (HBRBC_JIT_NET, A/B).
@@ -704,31 +706,34 @@ int spec_lds_stage() {
     if (const char *e = getenv("HBRBC_JIT_LDS_STAGE")) return std::max(1, std::min(32, atoi(e)));
     return 0;
 }
-int spec_wpe() {
+// waves/SIMD the LDS form targets: 7-row passes hold 56 accumulators, so
+// 128 VGPRs (4 waves/SIMD) fit without spills (r3 A/B)
+int spec_wpe(size_t nin, size_t nout) {
     if (const char *e = getenv("HBRBC_JIT_WPE")) return std::max(0, std::min(8, atoi(e)));
-    return 0;
+    return spec_lds(nin, nout) ? 4 : 0;
 }
 
 // Code-object name suffix of the variant options above (only where they
 // change the generated code: the LDS form needs 2..8 passes).
-std::string spec_suffix(size_t nout, int rt) {
+std::string spec_suffix(size_t nin, size_t nout, int rt) {
     const int npass = (int)((nout + rt - 1) / rt);
     std::string s;
-    if (spec_lds() && npass >= 2 && npass <= 8) {
+    if (spec_lds(nin, nout) && npass >= 2 && npass <= 8) {
         s += "_L";
         if (spec_lds_stage()) s += std::to_string(spec_lds_stage());
     }
     if (spec_net()) s += "_n" + std::to_string(spec_net());
-    if (spec_wpe()) s += "_w" + std::to_string(spec_wpe());
+    if (spec_wpe(nin, nout)) s += "_w" + std::to_string(spec_wpe(nin, nout));
     return s;
 }
 
 void spec_variant(XorProgram &p) {
-    p.lds = spec_lds();
+    const size_t nin = p.in_rows.size(), nout = p.out_rows.size();
+    p.lds = spec_lds(nin, nout);
     p.lds_stage = spec_lds_stage();
     p.net = spec_net();
-    p.wpe = spec_wpe();
-    p.name += spec_suffix(p.out_rows.size(), p.rt);
+    p.wpe = spec_wpe(nin, nout);
+    p.name += spec_suffix(nin, nout, p.rt);
 }
 
 bool read_file(const std::string &path, std::vector<char> &out) {
@@ -757,6 +762,9 @@ bool write_file(const std::string &path, const std::vector<char> &code) {
 int spec_row_tile(size_t nin, size_t nout) {
     // (passes are balanced: rt is the longest pass; HBRBC_RT_SPEC overrides, A/B)
     if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(24, atoi(e)));
+    // LDS form: passes no longer transpose their own inputs, so short passes
+    // (7 rows, nibble-subset network, <= 128 VGPRs) cost no extra transposes
+    if (spec_lds(nin, nout)) return 7;
     // split matrices (N = 250): 12-row passes of the pairwise network, four
     // per 48-row program (cfg5 encode 14.7 -> 12.4 ms, worst-case
     // reconstruct 13.1 -> 11.4 ms against 8-row nibble passes; 16 rows:
@@ -923,10 +931,11 @@ hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, X
 // 2.29x the algorithmic bytes, profiles/pmc_traffic.json); launched
 // concurrently on side streams they walk the instances together, so each
 // input row is fetched once and served to the other programs from L2 /
-// MALL.  HBRBC_XOR_STREAMS=0 keeps the serial order (A/B).
-bool xor_streams() {
+// MALL -- in theory; measured flat (cfg5 encode 11.9 vs 12.1 ms, reconstruct
+// 11.2 vs 11.5 ms, r3), so HBRBC_XOR_STREAMS=1 enables it for A/B only.
+bool xor_streams() {   // measured no gain (cfg5 73.7 vs 73.2 GB/s, r3): off by default
     const char *e = getenv("HBRBC_XOR_STREAMS");
-    return !(e && !std::strcmp(e, "0"));
+    return e && !std::strcmp(e, "1");
 }
 
 hipError_t launch_groups(hbrbc_ctx *c, const std::vector<hbrbc_ctx::SpecGroup> &gs, size_t first,
@@ -2010,7 +2019,8 @@ int hbrbc_jit_encode_file_name(size_t data_shards, size_t parity_shards, size_t 
                                         groups[group].first, groups[group].second, rb,
                                         spec_sync(), spec_fdepth(), spec_spread(),
                                         spec_split()) +
-                     spec_suffix(groups[group].second - groups[group].first, rt)).substr(1);
+                     spec_suffix(data_shards, groups[group].second - groups[group].first, rt))
+            .substr(1);
     if (f.size() + 1 > buf_len) return fail(HBRBC_E_INVALID_ARG, "buffer too small");
     std::memcpy(buf, f.c_str(), f.size() + 1);
     return HBRBC_OK;
