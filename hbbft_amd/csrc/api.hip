@@ -691,7 +691,9 @@ int spec_sync() {
 // profiles/r3_enc_variants.txt); HBRBC_JIT_LDS=0/1 overrides (A/B).
 bool spec_lds(size_t nin, size_t nout) {
     if (const char *e = getenv("HBRBC_JIT_LDS")) return !std::strcmp(e, "1");
-    return nin >= 16 && nin <= 32 && nout >= 14;
+    // cfg4 (k = 44): encode 4.41 -> 2.92 ms; cfg5 (k = 84, four programs):
+    // encode 12.11 -> 9.89, worst-case reconstruct 11.28 -> 9.08 ms (r3 A/B)
+    return nin >= 16 && nout >= 14;
 }
 
 // XOR-network form: 0 auto, 1 pairwise, 2 nibble-subset (HBRBC_JIT_NET, A/B).
@@ -708,9 +710,12 @@ int spec_lds_stage() {
 }
 // waves/SIMD the LDS form targets: 7-row passes hold 56 accumulators, so
 // 128 VGPRs (4 waves/SIMD) fit without spills (r3 A/B)
+int spec_row_tile(size_t nin, size_t nout);
 int spec_wpe(size_t nin, size_t nout) {
     if (const char *e = getenv("HBRBC_JIT_WPE")) return std::max(0, std::min(8, atoi(e)));
-    return spec_lds(nin, nout) ? 4 : 0;
+    if (!spec_lds(nin, nout)) return 0;
+    // <= 8-row passes: 128 VGPRs (4 waves/SIMD); 9..11-row passes: 168 (3)
+    return spec_row_tile(nin, nout) <= 8 ? 4 : 3;
 }
 
 // Code-object name suffix of the variant options above (only where they
@@ -763,8 +768,13 @@ int spec_row_tile(size_t nin, size_t nout) {
     // (passes are balanced: rt is the longest pass; HBRBC_RT_SPEC overrides, A/B)
     if (const char *e = getenv("HBRBC_RT_SPEC")) return std::max(2, std::min(24, atoi(e)));
     // LDS form: passes no longer transpose their own inputs, so short passes
-    // (7 rows, nibble-subset network, <= 128 VGPRs) cost no extra transposes
-    if (spec_lds(nin, nout)) return 7;
+    // (7 rows, nibble-subset network, <= 128 VGPRs) cost no extra transposes;
+    // a one-program matrix with more than 56 outputs takes longer passes so
+    // that one workgroup holds them all (<= 8 waves; cfg4: 84 rows, 11 per pass)
+    if (spec_lds(nin, nout)) {
+        if (nin * nout > 4096) return 7;   // split programs: groups of <= 48 rows
+        return (int)std::max<size_t>(7, (nout + 7) / 8);
+    }
     // split matrices (N = 250): 12-row passes of the pairwise network, four
     // per 48-row program (cfg5 encode 14.7 -> 12.4 ms, worst-case
     // reconstruct 13.1 -> 11.4 ms against 8-row nibble passes; 16 rows:

@@ -1070,16 +1070,21 @@ size_t shaped_lds(size_t lanes, int max_w, size_t static_lds = 0) {
 constexpr int kSpongeMaxWaves = 4;  // VGPR-limited residency of the sponge kernels (<= 128 VGPRs)
 // Grids below 2^18 sponges (< 4 waves per SIMD) take the 16-byte-load variant.
 bool few_sponges(size_t lanes) { return lanes < ((size_t)1 << 18); }
-// Pair-lane sponges (two lanes each): HBRBC_SPONGE_PAIR=1 always, =2 for
-// grids below `pair_below` sponges, 0 never (default; A/B).
+// Pair-lane sponges (two lanes each, ~33 % more VALU per sponge): for grids
+// far below one wave per SIMD, where a sponge's serial permutation chain --
+// not issue -- sets the time.  Per-call Proof::validate 925 -> 651 us (cfg3
+// shard), 3831 -> 2361 us (cfg5); at 65536 sponges (cfg2 leaf hash, one wave
+// per SIMD) 22.8 -> 31.5 ms, so only grids below 16384 sponges (r3 A/B,
+// profiles/r3_percall.jsonl).  HBRBC_SPONGE_PAIR=0 never, 1 always, 2 below
+// HBRBC_SPONGE_PAIR_BELOW sponges (default 2, 16384).
 bool pair_sponges(size_t sponges) {
     static const int mode = [] {
         const char *e = getenv("HBRBC_SPONGE_PAIR");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 2;
     }();
     static const size_t below = [] {
         const char *e = getenv("HBRBC_SPONGE_PAIR_BELOW");
-        return e ? (size_t)atoll(e) : ((size_t)1 << 17);
+        return e ? (size_t)atoll(e) : (size_t)16384;
     }();
     return mode == 1 || (mode == 2 && sponges < below);
 }
