@@ -83,12 +83,23 @@ struct Sm {
     size_t inst;
     int me, proposer, role;
     bool drop;                // a silent node's deliveries emit nothing
-    // state of (inst, me)
-    uint16_t *echo;
-    uint8_t *ready;
-    uint32_t *cand;           // [C][W]
-    uint16_t *cnt_e, *cnt_f, *cnt_r;   // [C] each
-    uint32_t *flags;
+    // state of (inst, me), structure of arrays over the instance's hosted
+    // nodes (stride sd = nodes): the nodes of an instance are consecutive
+    // threads, so every state access of a wave is one coalesced request
+    uint16_t *echo;           // [n][sd]
+    uint8_t *ready;           // [n][sd]
+    uint32_t *cand;           // [C][W][sd]
+    uint16_t *cnt;            // [3][C][sd]: Echo+EchoHash, full Echo, Ready counts
+    uint32_t *flags;          // [sd]
+    size_t sd;
+
+    __device__ uint16_t &ECHO(int s) { return echo[(size_t)s * sd]; }
+    __device__ uint8_t &READY(int s) { return ready[(size_t)s * sd]; }
+    __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
+    __device__ uint16_t &CE(uint32_t c) { return cnt[(size_t)c * sd]; }
+    __device__ uint16_t &CF(uint32_t c) { return cnt[((size_t)C + c) * sd]; }
+    __device__ uint16_t &CR(uint32_t c) { return cnt[((size_t)2 * C + c) * sd]; }
+    __device__ uint32_t &FLAGS() { return *flags; }
     uint32_t *out;            // [max_out][rec]
     uint32_t nout;
     bool overflow;
@@ -135,9 +146,9 @@ struct Sm {
 
     // -- handlers (broadcast.rs) --------------------------------------------
     __device__ void compute_output(uint32_t c) {   // 526-558
-        if ((*flags & FL_DECIDED) || cnt_r[c] <= 2 * f || cnt_f[c] < k) return;
+        if ((FLAGS() & FL_DECIDED) || CR(c) <= 2 * f || CF(c) < k) return;
         if (a.decode_ok[inst * C + c]) {
-            *flags |= FL_DECIDED;
+            FLAGS() |= FL_DECIDED;
             a.output_root[inst * a.nodes + (me - a.node_lo)] = (uint8_t)c;
         } else {
             fault(proposer, F_BROADCAST_DECODING);
@@ -145,20 +156,20 @@ struct Sm {
     }
 
     __device__ void send_echo_remaining(uint32_t c) {   // 428-453
-        *flags |= FL_ECHO_SENT;
-        const uint32_t e = echo[me];
+        FLAGS() |= FL_ECHO_SENT;
+        const uint32_t e = ECHO(me);
         if (!is_full(e) || root_of(e) != c) return;
         uint32_t *r = emit(K_ECHO, c, e & 0xFFu, (e >> 13) & 1u);
         if (!r) return;
-        const uint32_t *cd = cand + (size_t)c * W;
         for (int i = 0; i < n; ++i)
-            if (is_right_of(i, me) && !bit(cd, i)) r[1 + (i >> 5)] |= 1u << (i & 31);
+            if (is_right_of(i, me) && !((CAND(c, i >> 5) >> (i & 31)) & 1u))
+                r[1 + (i >> 5)] |= 1u << (i & 31);
     }
 
     __device__ void handle_ready_core(int s, uint32_t c, bool may_send);
 
     __device__ void send_ready(uint32_t c) {   // 513-522
-        *flags |= FL_READY_SENT;
+        FLAGS() |= FL_READY_SENT;
         uint32_t *r = emit(K_READY, c);
         if (r)
             for (int i = 0; i < n; ++i)
@@ -167,20 +178,20 @@ struct Sm {
     }
 
     __device__ void handle_can_decode(int s, uint32_t c) {   // 358-375
-        cand[(size_t)c * W + (s >> 5)] |= 1u << (s & 31);
+        CAND(c, s >> 5) |= 1u << (s & 31);
     }
 
     __device__ void send_can_decode(uint32_t c) {   // 488-510
-        *flags |= 1u << (FL_CAN_DECODE_SHIFT + c);
+        FLAGS() |= 1u << (FL_CAN_DECODE_SHIFT + c);
         uint32_t *r = emit(K_CAN_DECODE, c);
         if (r)
             for (int i = 0; i < n; ++i)
-                if (i != me && !is_full(echo[i])) r[1 + (i >> 5)] |= 1u << (i & 31);
+                if (i != me && !is_full(ECHO(i))) r[1 + (i >> 5)] |= 1u << (i & 31);
         handle_can_decode(me, c);
     }
 
     __device__ void handle_echo(int s, uint32_t c, uint32_t j, uint32_t t) {   // 266-320
-        const uint32_t e = echo[s];
+        const uint32_t e = ECHO(s);
         if (is_full(e)) {
             if (e != enc_full(c, j, t)) fault(s, F_MULTIPLE_ECHOS);
             return;
@@ -193,23 +204,23 @@ struct Sm {
             fault(s, F_INVALID_PROOF);
             return;
         }
-        if (!e) ++cnt_e[c];   // a Hash of the same root was counted already
-        ++cnt_f[c];
-        echo[s] = (uint16_t)enc_full(c, j, t);
-        if (!(*flags & (1u << (FL_CAN_DECODE_SHIFT + c))) && cnt_f[c] >= k) send_can_decode(c);
-        if (!(*flags & FL_READY_SENT) && cnt_e[c] >= n - f) send_ready(c);
-        if (*flags & FL_READY_SENT) compute_output(c);
+        if (!e) ++CE(c);   // a Hash of the same root was counted already
+        ++CF(c);
+        ECHO(s) = (uint16_t)enc_full(c, j, t);
+        if (!(FLAGS() & (1u << (FL_CAN_DECODE_SHIFT + c))) && CF(c) >= k) send_can_decode(c);
+        if (!(FLAGS() & FL_READY_SENT) && CE(c) >= n - f) send_ready(c);
+        if (FLAGS() & FL_READY_SENT) compute_output(c);
     }
 
     __device__ void handle_echo_hash(int s, uint32_t c) {   // 322-355
-        const uint32_t e = echo[s];
+        const uint32_t e = ECHO(s);
         if (e) {
             if (root_of(e) != c) fault(s, F_MULTIPLE_ECHO_HASHES);
             return;
         }
-        echo[s] = (uint16_t)enc_hash(c);
-        ++cnt_e[c];
-        if ((*flags & FL_READY_SENT) || cnt_e[c] < n - f) {
+        ECHO(s) = (uint16_t)enc_hash(c);
+        ++CE(c);
+        if ((FLAGS() & FL_READY_SENT) || CE(c) < n - f) {
             compute_output(c);
             return;
         }
@@ -217,7 +228,7 @@ struct Sm {
     }
 
     __device__ void send_echo_hash(uint32_t c) {   // 456-468
-        *flags |= FL_ECHO_HASH_SENT;
+        FLAGS() |= FL_ECHO_HASH_SENT;
         uint32_t *r = emit(K_ECHO_HASH, c);
         if (r)
             for (int i = 0; i < n; ++i)
@@ -263,7 +274,7 @@ struct Sm {
             fault(s, F_VALUE_FROM_NON_PROPOSER);
             return;
         }
-        const uint32_t e = echo[me];
+        const uint32_t e = ECHO(me);
         if (e) {
             if (root_of(e) != c) {
                 fault(s, F_MULTIPLE_VALUES);
@@ -322,16 +333,16 @@ struct Sm {
 };
 
 __device__ void Sm::handle_ready_core(int s, uint32_t c, bool may_send) {   // 378-410
-    const uint32_t old = ready[s];
+    const uint32_t old = READY(s);
     if (old) {
         if (old - 1 != c) fault(s, F_MULTIPLE_READYS);
         return;
     }
-    ready[s] = (uint8_t)(c + 1);
-    ++cnt_r[c];
+    READY(s) = (uint8_t)(c + 1);
+    ++CR(c);
     // (from send_ready, ready_sent is already set: no further send_ready)
-    if (may_send && cnt_r[c] == f + 1 && !(*flags & FL_READY_SENT)) send_ready(c);
-    if (cnt_r[c] == 2 * f + 1) send_echo_remaining(c);
+    if (may_send && CR(c) == f + 1 && !(FLAGS() & FL_READY_SENT)) send_ready(c);
+    if (CR(c) == 2 * f + 1) send_echo_remaining(c);
     compute_output(c);
 }
 
@@ -343,8 +354,9 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     const int me = (int)a.node_lo + local;
     if (me >= n) return;
     const int W = (n + 31) / 32, C = (int)a.roots;
-    const size_t sb = sm_state_bytes(n, a.roots);
-    uint8_t *st = a.state + g * sb;
+    // this instance's state block (nodes x sm_state_bytes), structure of arrays
+    const size_t sd = a.nodes;
+    uint8_t *st = a.state + inst * sd * sm_state_bytes(n, a.roots);
     Sm m{a};
     m.n = n;
     m.f = f;
@@ -356,14 +368,15 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     m.me = me;
     m.proposer = a.proposer[inst];
     m.role = a.role[inst * n + me];
-    m.echo = reinterpret_cast<uint16_t *>(st);
-    m.ready = st + 2 * (size_t)n;
-    const size_t o_cand = (3 * (size_t)n + 3) & ~(size_t)3;
-    m.cand = reinterpret_cast<uint32_t *>(st + o_cand);
-    m.cnt_e = reinterpret_cast<uint16_t *>(st + o_cand + 4 * (size_t)C * W);
-    m.cnt_f = m.cnt_e + C;
-    m.cnt_r = m.cnt_f + C;
-    m.flags = reinterpret_cast<uint32_t *>(st + ((o_cand + 4 * (size_t)C * W + 6 * (size_t)C + 3) & ~(size_t)3));
+    m.sd = sd;
+    m.echo = reinterpret_cast<uint16_t *>(st) + local;
+    m.ready = st + 2 * (size_t)n * sd + local;
+    const size_t o_cand = (3 * (size_t)n * sd + 3) & ~(size_t)3;
+    m.cand = reinterpret_cast<uint32_t *>(st + o_cand) + local;
+    const size_t o_cnt = o_cand + 4 * (size_t)C * W * sd;
+    m.cnt = reinterpret_cast<uint16_t *>(st + o_cnt) + local;
+    const size_t o_flags = (o_cnt + 6 * (size_t)C * sd + 3) & ~(size_t)3;
+    m.flags = reinterpret_cast<uint32_t *>(st + o_flags) + local;
     m.out = a.out + g * (size_t)a.max_out * (1 + W);
     m.nout = 0;
     m.overflow = false;
