@@ -505,6 +505,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     timer.reset()
     timer.timing = world > 1
     ex.reset_stats()
+    sb.sm_timing = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -517,6 +518,8 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     elapsed = time.perf_counter() - t0
     for s_ in subs:
         s_.rb.profile(False)
+    sm_ms = sum(e0.elapsed_time(e1) for e0, e1 in sb.sm_timing) / args.steps
+    sb.sm_timing = None
     elapsed = max_over_ranks(elapsed, world, dev)
     xms = timer.elapsed_ms() / args.steps if world > 1 else 0.0
     timer.timing = False
@@ -565,7 +568,8 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                      "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
                      "backend": ex.backend, "per_rank": per_rank},
         "work_per_step_rank0": counts,
-        "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
+        "stages_ms_per_step": dict({s: stages[s][0] / args.steps for s in stages},
+                                   state_machine=sm_ms),
     }
 
 

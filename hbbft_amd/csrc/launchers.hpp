@@ -249,15 +249,13 @@ hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_ou
 
 hipError_t configure_kernels();
 
-// Broadcast state machine rounds (sim.hip).  Bytes per node: echo u16[n],
-// ready u8[n], can_decodes u32[roots][W], counters u16[3][roots], flags u32
-// (+8 of alignment slack); an instance's block holds its hosted nodes'
-// fields as structures of arrays.
+// Broadcast state machine rounds (sim.hip).  Bytes per node: er u16[n]
+// (echo | ready << 8), can_decodes u32[roots][W], counters u16[3][roots],
+// flags u32, + 6 of alignment slack for a block, rounded to 8; an instance's
+// block holds its hosted nodes' fields as structures of arrays.
 __host__ __device__ inline size_t sm_state_bytes(size_t n, size_t roots) {
     const size_t w = (n + 31) / 32;
-    const size_t cand = (3 * n + 3) & ~(size_t)3;
-    const size_t flags = (cand + 4 * roots * w + 6 * roots + 3) & ~(size_t)3;
-    return (flags + 4 + 8 + 7) & ~(size_t)7;
+    return (2 * n + 4 * roots * w + 6 * roots + 4 + 6 + 7) & ~(size_t)7;
 }
 hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s);
 

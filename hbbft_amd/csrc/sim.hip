@@ -37,6 +37,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 namespace hbrbc {
 
 namespace {
@@ -67,15 +70,18 @@ enum : uint32_t {
     FL_CAN_DECODE_SHIFT = 8u,   // bits 8..15: can_decode_sent per root
 };
 
-// echo entry (EchoContent): 0 none; Hash: 0x4000 | c << 8; Full: 0x8000 |
-// t << 13 | c << 8 | index
-__device__ __forceinline__ uint32_t enc_full(uint32_t c, uint32_t j, uint32_t t) {
-    return 0x8000u | (t << 13) | (c << 8) | j;
+// Per sender s a node keeps one 16-bit word (er[s]): bits 0..7 the echo
+// entry (EchoContent) -- 0 none, Hash: 0x10 | c, Full: 0x20 | t << 3 | c (a
+// stored full Echo is always proof index s, validate_proof checks it) -- and
+// bits 8..11 the Ready entry (root + 1, 0 none).
+__device__ __forceinline__ uint32_t enc_full(uint32_t c, uint32_t t) {
+    return 0x20u | ((t & 1u) << 3) | (c & 7u);
 }
-__device__ __forceinline__ uint32_t enc_hash(uint32_t c) { return 0x4000u | (c << 8); }
-__device__ __forceinline__ bool is_full(uint32_t e) { return e & 0x8000u; }
-__device__ __forceinline__ bool is_hash(uint32_t e) { return e & 0x4000u; }
-__device__ __forceinline__ uint32_t root_of(uint32_t e) { return (e >> 8) & 31u; }
+__device__ __forceinline__ uint32_t enc_hash(uint32_t c) { return 0x10u | (c & 7u); }
+__device__ __forceinline__ bool is_full(uint32_t e) { return e & 0x20u; }
+__device__ __forceinline__ bool is_hash(uint32_t e) { return e & 0x10u; }
+__device__ __forceinline__ uint32_t root_of(uint32_t e) { return e & 7u; }
+__device__ __forceinline__ uint32_t tamper_of(uint32_t e) { return (e >> 3) & 1u; }
 
 struct Sm {
     const hbrbc_sm_args &a;
@@ -86,15 +92,24 @@ struct Sm {
     // state of (inst, me), structure of arrays over the instance's hosted
     // nodes (stride sd = nodes): the nodes of an instance are consecutive
     // threads, so every state access of a wave is one coalesced request
-    uint16_t *echo;           // [n][sd]
-    uint8_t *ready;           // [n][sd]
+    uint16_t *er;             // [n][sd]: echo entry | ready entry << 8
     uint32_t *cand;           // [C][W][sd]
     uint16_t *cnt;            // [3][C][sd]: Echo+EchoHash, full Echo, Ready counts
     uint32_t *flags;          // [sd]
     size_t sd;
+    const uint8_t *pok;       // this instance's proof_ok [C][2][n]
+    const uint8_t *dok;       // this instance's decode_ok [C]
 
-    __device__ uint16_t &ECHO(int s) { return echo[(size_t)s * sd]; }
-    __device__ uint8_t &READY(int s) { return ready[(size_t)s * sd]; }
+    __device__ uint32_t ECHO(int s) const { return er[(size_t)s * sd] & 0xFFu; }
+    __device__ void set_echo(int s, uint32_t e) {
+        uint16_t &w = er[(size_t)s * sd];
+        w = (uint16_t)((w & 0xFF00u) | e);
+    }
+    __device__ uint32_t READY(int s) const { return er[(size_t)s * sd] >> 8; }
+    __device__ void set_ready(int s, uint32_t r) {
+        uint16_t &w = er[(size_t)s * sd];
+        w = (uint16_t)((w & 0xFFu) | (r << 8));
+    }
     __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
     __device__ uint16_t &CE(uint32_t c) { return cnt[(size_t)c * sd]; }
     __device__ uint16_t &CF(uint32_t c) { return cnt[((size_t)C + c) * sd]; }
@@ -127,8 +142,20 @@ struct Sm {
         uint32_t *r = out + (size_t)nout * rec;
         ++nout;
         r[0] = kind | (c << 8) | (j << 16) | (t << 24);
-        for (int w = 0; w < W; ++w) r[1 + w] = 0;
         return r;
+    }
+
+    // the recipient mask of record r: bit i set iff pred(i), each word built
+    // in a register and stored once (the caller fills every emitted record)
+    template <class P>
+    __device__ void targets(uint32_t *r, P pred) {
+        for (int w = 0; w < W; ++w) {
+            uint32_t mk = 0;
+            const int hi = n - 32 * w < 32 ? n - 32 * w : 32;
+            for (int b = 0; b < hi; ++b)
+                if (pred(32 * w + b)) mk |= 1u << b;
+            r[1 + w] = mk;
+        }
     }
 
     // emission as the node's own step (subject to its role)
@@ -141,13 +168,13 @@ struct Sm {
 
     __device__ bool validate_proof(uint32_t c, uint32_t j, uint32_t t, int sender) const {
         if ((int)j != sender || c >= (uint32_t)C || j >= (uint32_t)n) return false;
-        return a.proof_ok[((inst * C + c) * 2 + (t & 1)) * n + j] != 0;
+        return pok[(c * 2 + (t & 1)) * n + j] != 0;
     }
 
     // -- handlers (broadcast.rs) --------------------------------------------
     __device__ void compute_output(uint32_t c) {   // 526-558
         if ((FLAGS() & FL_DECIDED) || CR(c) <= 2 * f || CF(c) < k) return;
-        if (a.decode_ok[inst * C + c]) {
+        if (dok[c]) {
             FLAGS() |= FL_DECIDED;
             a.output_root[inst * a.nodes + (me - a.node_lo)] = (uint8_t)c;
         } else {
@@ -159,11 +186,9 @@ struct Sm {
         FLAGS() |= FL_ECHO_SENT;
         const uint32_t e = ECHO(me);
         if (!is_full(e) || root_of(e) != c) return;
-        uint32_t *r = emit(K_ECHO, c, e & 0xFFu, (e >> 13) & 1u);
+        uint32_t *r = emit(K_ECHO, c, (uint32_t)me, tamper_of(e));
         if (!r) return;
-        for (int i = 0; i < n; ++i)
-            if (is_right_of(i, me) && !((CAND(c, i >> 5) >> (i & 31)) & 1u))
-                r[1 + (i >> 5)] |= 1u << (i & 31);
+        targets(r, [&](int i) { return is_right_of(i, me) && !((CAND(c, i >> 5) >> (i & 31)) & 1u); });
     }
 
     __device__ void handle_ready_core(int s, uint32_t c, bool may_send);
@@ -171,9 +196,7 @@ struct Sm {
     __device__ void send_ready(uint32_t c) {   // 513-522
         FLAGS() |= FL_READY_SENT;
         uint32_t *r = emit(K_READY, c);
-        if (r)
-            for (int i = 0; i < n; ++i)
-                if (i != me) r[1 + (i >> 5)] |= 1u << (i & 31);
+        if (r) targets(r, [&](int i) { return i != me; });
         handle_ready_core(me, c, false);
     }
 
@@ -184,16 +207,14 @@ struct Sm {
     __device__ void send_can_decode(uint32_t c) {   // 488-510
         FLAGS() |= 1u << (FL_CAN_DECODE_SHIFT + c);
         uint32_t *r = emit(K_CAN_DECODE, c);
-        if (r)
-            for (int i = 0; i < n; ++i)
-                if (i != me && !is_full(ECHO(i))) r[1 + (i >> 5)] |= 1u << (i & 31);
+        if (r) targets(r, [&](int i) { return i != me && !is_full(ECHO(i)); });
         handle_can_decode(me, c);
     }
 
     __device__ void handle_echo(int s, uint32_t c, uint32_t j, uint32_t t) {   // 266-320
         const uint32_t e = ECHO(s);
-        if (is_full(e)) {
-            if (e != enc_full(c, j, t)) fault(s, F_MULTIPLE_ECHOS);
+        if (is_full(e)) {   // the stored proof is (root_of(e), s, tamper_of(e))
+            if (e != enc_full(c, t) || (int)j != s) fault(s, F_MULTIPLE_ECHOS);
             return;
         }
         if (is_hash(e) && root_of(e) != c) {
@@ -206,7 +227,7 @@ struct Sm {
         }
         if (!e) ++CE(c);   // a Hash of the same root was counted already
         ++CF(c);
-        ECHO(s) = (uint16_t)enc_full(c, j, t);
+        set_echo(s, enc_full(c, t));
         if (!(FLAGS() & (1u << (FL_CAN_DECODE_SHIFT + c))) && CF(c) >= k) send_can_decode(c);
         if (!(FLAGS() & FL_READY_SENT) && CE(c) >= n - f) send_ready(c);
         if (FLAGS() & FL_READY_SENT) compute_output(c);
@@ -218,7 +239,7 @@ struct Sm {
             if (root_of(e) != c) fault(s, F_MULTIPLE_ECHO_HASHES);
             return;
         }
-        ECHO(s) = (uint16_t)enc_hash(c);
+        set_echo(s, enc_hash(c));
         ++CE(c);
         if ((FLAGS() & FL_READY_SENT) || CE(c) < n - f) {
             compute_output(c);
@@ -230,17 +251,13 @@ struct Sm {
     __device__ void send_echo_hash(uint32_t c) {   // 456-468
         FLAGS() |= FL_ECHO_HASH_SENT;
         uint32_t *r = emit(K_ECHO_HASH, c);
-        if (r)
-            for (int i = 0; i < n; ++i)
-                if (is_right_of(i, me)) r[1 + (i >> 5)] |= 1u << (i & 31);
+        if (r) targets(r, [&](int i) { return is_right_of(i, me); });
         handle_echo_hash(me, c);
     }
 
     __device__ void send_echo_left(uint32_t c, uint32_t j, uint32_t t) {   // 413-425
         uint32_t *r = emit(K_ECHO, c, j, t);
-        if (r)
-            for (int i = 0; i < n; ++i)
-                if (i != me && !is_right_of(i, me)) r[1 + (i >> 5)] |= 1u << (i & 31);
+        if (r) targets(r, [&](int i) { return i != me && !is_right_of(i, me); });
         handle_echo(me, c, j, t);
     }
 
@@ -280,7 +297,7 @@ struct Sm {
                 fault(s, F_MULTIPLE_VALUES);
                 return;
             }
-            if (is_full(e) && e == enc_full(c, j, t)) return;
+            if (is_full(e) && e == enc_full(c, t)) return;   // j == me: the stored index
         }
         if (!validate_proof(c, j, t, me)) {
             fault(s, F_INVALID_PROOF);
@@ -338,7 +355,7 @@ __device__ void Sm::handle_ready_core(int s, uint32_t c, bool may_send) {   // 3
         if (old - 1 != c) fault(s, F_MULTIPLE_READYS);
         return;
     }
-    READY(s) = (uint8_t)(c + 1);
+    set_ready(s, c + 1);
     ++CR(c);
     // (from send_ready, ready_sent is already set: no further send_ready)
     if (may_send && CR(c) == f + 1 && !(FLAGS() & FL_READY_SENT)) send_ready(c);
@@ -346,17 +363,31 @@ __device__ void Sm::handle_ready_core(int s, uint32_t c, bool may_send) {   // 3
     compute_output(c);
 }
 
-__global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, int f, int k) {
-    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (g >= a.count * a.nodes) return;
-    const size_t inst = g / a.nodes;
-    const int local = (int)(g - inst * a.nodes);
+
+// Byte offsets of the fields of an instance's state block holding `sd` nodes
+// as structures of arrays (include/hbrbc.h hbrbc_sm_state_bytes, per node:
+// er u16[n], cand u32[C][W], counters u16[3][C], flags u32).
+struct SmLayout {
+    size_t er, cand, cnt, flags;
+    __device__ SmLayout(int n, int C, int W, size_t sd) {
+        er = 0;
+        cand = (2 * (size_t)n * sd + 3) & ~(size_t)3;
+        cnt = cand + 4 * (size_t)C * W * sd;
+        flags = (cnt + 6 * (size_t)C * sd + 3) & ~(size_t)3;
+    }
+};
+
+// Handles one node's inbox of the round (or, in round 0, the proposer's
+// broadcast()).  `st` is the instance's state block (stride sd = nodes),
+// `inc(s)` sender s's record count, `recs(s)` its records.
+template <class InCount, class Recs>
+__device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
+                        int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
+                        InCount inc, Recs recs) {
     const int me = (int)a.node_lo + local;
-    if (me >= n) return;
     const int W = (n + 31) / 32, C = (int)a.roots;
-    // this instance's state block (nodes x sm_state_bytes), structure of arrays
     const size_t sd = a.nodes;
-    uint8_t *st = a.state + inst * sd * sm_state_bytes(n, a.roots);
+    const SmLayout L(n, C, W, sd);
     Sm m{a};
     m.n = n;
     m.f = f;
@@ -369,14 +400,12 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     m.proposer = a.proposer[inst];
     m.role = a.role[inst * n + me];
     m.sd = sd;
-    m.echo = reinterpret_cast<uint16_t *>(st) + local;
-    m.ready = st + 2 * (size_t)n * sd + local;
-    const size_t o_cand = (3 * (size_t)n * sd + 3) & ~(size_t)3;
-    m.cand = reinterpret_cast<uint32_t *>(st + o_cand) + local;
-    const size_t o_cnt = o_cand + 4 * (size_t)C * W * sd;
-    m.cnt = reinterpret_cast<uint16_t *>(st + o_cnt) + local;
-    const size_t o_flags = (o_cnt + 6 * (size_t)C * sd + 3) & ~(size_t)3;
-    m.flags = reinterpret_cast<uint32_t *>(st + o_flags) + local;
+    m.er = reinterpret_cast<uint16_t *>(st + L.er) + local;
+    m.cand = reinterpret_cast<uint32_t *>(st + L.cand) + local;
+    m.cnt = reinterpret_cast<uint16_t *>(st + L.cnt) + local;
+    m.flags = reinterpret_cast<uint32_t *>(st + L.flags) + local;
+    m.pok = pok;
+    m.dok = dok;
     m.out = a.out + g * (size_t)a.max_out * (1 + W);
     m.nout = 0;
     m.overflow = false;
@@ -391,31 +420,26 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
             *m.flags |= FL_VALUE_SENT;
             uint32_t *r = m.emit_rec(K_VALUE, kNone, 0, 0);
             if (r)
-                for (int i = 0; i < n; ++i)
-                    if (i != me && a.value_root[inst * n + i] != kNone) r[1 + (i >> 5)] |= 1u << (i & 31);
+                m.targets(r, [&](int i) { return i != me && a.value_root[inst * n + i] != kNone; });
             const uint32_t c = a.value_root[inst * n + me];
             if (c != kNone) m.handle_value(me, c, (uint32_t)me, a.value_tamper[inst * n + me]);
         }
     } else {
         m.drop = m.role == R_SILENT;
-        const uint32_t R = a.rows_per_rank;
         const bool faker = a.fake_from[inst] == (uint8_t)me;
         for (int s = 0; s < n; ++s) {
             if (s == me) continue;   // targets never include the sender
-            const size_t blk = ((size_t)(s / R) * a.count + inst) * R + (s % R);
-            const uint32_t cnt = a.in_count[blk] & 0x7FFFFFFFu;
-            const uint32_t *recs = a.in + blk * (size_t)a.max_out * (1 + W);
-            for (uint32_t e = 0; e < cnt && e < a.max_out; ++e) {
-                const uint32_t *r = recs + (size_t)e * (1 + W);
+            const uint32_t cnt = inc(s);
+            const uint32_t *rs = recs(s);
+            for (uint32_t e = 0; e < cnt; ++e) {
+                const uint32_t *r = rs + (size_t)e * (1 + W);
                 if (!m.bit(r + 1, me)) continue;
                 m.deliver(s, r);
                 if (faker && !(*m.flags & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
                     *m.flags |= FL_FAKE_DONE;
                     uint32_t *fr = m.emit_rec(K_FAKE, a.fake_root[inst], 0, 0);
-                    if (fr)
-                        for (int i = 0; i < n; ++i)
-                            if (i != me) fr[1 + (i >> 5)] |= 1u << (i & 31);
+                    if (fr) m.targets(fr, [&](int i) { return i != me; });
                 }
             }
         }
@@ -423,13 +447,120 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     a.out_count[g] = m.nout | (m.overflow ? 0x80000000u : 0u);
     a.fault_count[g] = m.nfault;
     if (m.nout) atomicAdd(a.emitted, m.nout);
+    if (m.overflow) atomicOr(a.emitted + 1, 1u);
+}
+
+__device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t inst, int s) {
+    const uint32_t R = a.rows_per_rank;
+    return ((size_t)(s / R) * a.count + inst) * R + (s % R);
+}
+
+// Round kernel, global form: one thread per (instance, hosted node), state,
+// records and outcomes read where they lie.  For blocks whose staged copy
+// does not fit the LDS budget (sm_plan).
+__global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, int f, int k) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (g >= a.count * a.nodes) return;
+    const size_t inst = g / a.nodes;
+    const int local = (int)(g - inst * a.nodes);
+    if ((int)a.node_lo + local >= n) return;
+    const size_t MR = (size_t)a.max_out * ((n + 31) / 32 + 1);
+    uint8_t *st = a.state + inst * a.nodes * sm_state_bytes(n, a.roots);
+    sm_node(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
+            a.decode_ok + inst * a.roots,
+            [&](int s) {
+                const uint32_t c = a.in_count[sm_in_block(a, inst, s)] & 0x7FFFFFFFu;
+                return c < a.max_out ? c : a.max_out;
+            },
+            [&](int s) { return a.in + sm_in_block(a, inst, s) * MR; });
+}
+
+// Round kernel, staged form: a workgroup owns `ipb` whole instances (ipb x
+// nodes threads) and first copies into LDS, cooperatively and coalesced,
+// their state blocks (contiguous in global memory), every sender's records
+// and counts of the round, and their proof / decode outcomes; the handlers'
+// dependent read-modify-write chains (handle_echo: entry, Echo count, full
+// count, flags, outcome, ...) then cost LDS latency instead of an L2 round
+// trip each.  The state goes back at the end.
+__global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
+                                                             int k, int ipb) {
+    extern __shared__ uint4 sm_lds4[];
+    uint8_t *lds = reinterpret_cast<uint8_t *>(sm_lds4);
+    const int T = (int)blockDim.x, tid = (int)threadIdx.x;
+    const size_t inst0 = (size_t)blockIdx.x * ipb;
+    const int ni = (int)((a.count - inst0) < (size_t)ipb ? (a.count - inst0) : (size_t)ipb);
+    const int W = (n + 31) / 32, C = (int)a.roots;
+    const size_t sb = sm_state_bytes(n, a.roots), nodes = a.nodes;
+    const size_t MR = (size_t)a.max_out * (1 + W);   // words per sender
+    // LDS: state [ipb][nodes * sb] | counts u32 [ipb][n] | records u32
+    // [ipb][n][MR] | proof_ok [ipb][C * 2 * n] | decode_ok [ipb][C]
+    const size_t o_cnt = (size_t)ipb * nodes * sb;   // sb % 8 == 0
+    const size_t o_rec = o_cnt + 4 * (size_t)ipb * n;
+    const size_t o_pok = o_rec + 4 * (size_t)ipb * n * MR;
+    const size_t o_dok = o_pok + (size_t)ipb * C * 2 * n;
+    uint8_t *gst = a.state + inst0 * nodes * sb;
+    const size_t st_words = (size_t)ni * nodes * sb / 8;
+    for (size_t i = tid; i < st_words; i += T)
+        reinterpret_cast<uint2 *>(lds)[i] = reinterpret_cast<const uint2 *>(gst)[i];
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(lds + o_cnt);
+    uint32_t *lrec = reinterpret_cast<uint32_t *>(lds + o_rec);
+    if (a.round > 0) {
+        for (int i = tid; i < ni * n; i += T) {
+            const int li = i / n, s = i - li * n;
+            const uint32_t c = a.in_count[sm_in_block(a, inst0 + li, s)] & 0x7FFFFFFFu;
+            lcnt[i] = c < a.max_out ? c : a.max_out;
+        }
+        // 32-bit index arithmetic (a 64-bit division is a long software loop)
+        const uint32_t mr = (uint32_t)MR, rw = (uint32_t)(ni * n) * mr;
+        for (uint32_t i = tid; i < rw; i += T) {
+            const uint32_t ls = i / mr, w = i - ls * mr;
+            const uint32_t li = ls / (uint32_t)n, s = ls - li * (uint32_t)n;
+            lrec[i] = a.in[sm_in_block(a, inst0 + li, (int)s) * MR + w];
+        }
+    }
+    const uint32_t pw = (uint32_t)(ni * C * 2 * n);
+    for (uint32_t i = tid; i < pw; i += T) lds[o_pok + i] = a.proof_ok[inst0 * C * 2 * n + i];
+    for (int i = tid; i < ni * C; i += T) lds[o_dok + i] = a.decode_ok[inst0 * C + i];
+    __syncthreads();
+    const int li = tid / (int)nodes, local = tid - li * (int)nodes;
+    if (li < ni && (int)a.node_lo + local < n) {
+        const size_t inst = inst0 + li;
+        const uint32_t *cb = lcnt + (size_t)li * n;
+        const uint32_t *rb = lrec + (size_t)li * n * MR;
+        sm_node(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
+                lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
+                [&](int s) { return cb[s]; }, [&](int s) { return rb + (size_t)s * MR; });
+    }
+    __syncthreads();
+    for (size_t i = tid; i < st_words; i += T)
+        reinterpret_cast<uint2 *>(gst)[i] = reinterpret_cast<const uint2 *>(lds)[i];
 }
 
 }  // namespace
 
+// Launch plan: the staged form with ipb instances per workgroup (ipb x nodes
+// <= 256 threads, at most 128 unless one instance needs more) when its LDS
+// image fits 64 KiB; else the global form.
+static size_t sm_lds_bytes(const hbrbc_sm_args &a, int n, int ipb) {
+    const size_t W = (n + 31) / 32, MR = (size_t)a.max_out * (1 + W);
+    const size_t per = a.nodes * sm_state_bytes(n, a.roots) + 4 * (size_t)n + 4 * (size_t)n * MR +
+                       (size_t)a.roots * 2 * n + a.roots;
+    return ((size_t)ipb * per + 15) & ~(size_t)15;
+}
+
 hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s) {
     const size_t threads = a.count * a.nodes;
     if (threads == 0) return hipSuccess;
+    const char *e = getenv("HBRBC_SM_STAGED");   // 0: the global form (A/B)
+    const bool staged_ok = !(e && !strcmp(e, "0")) && a.nodes <= 256;
+    int ipb = a.nodes >= 128 ? 1 : (int)(128 / a.nodes);
+    while (ipb > 1 && sm_lds_bytes(a, n, ipb) > 65536) --ipb;
+    if (staged_ok && sm_lds_bytes(a, n, ipb) <= 65536) {
+        const unsigned blocks = (unsigned)((a.count + ipb - 1) / ipb);
+        hipLaunchKernelGGL(sm_round_staged_kernel, dim3(blocks), dim3((unsigned)(ipb * a.nodes)),
+                           sm_lds_bytes(a, n, ipb), s, a, n, f, k, ipb);
+        return hipGetLastError();
+    }
     const unsigned blocks = (unsigned)((threads + 255) / 256);
     hipLaunchKernelGGL(sm_round_kernel, dim3(blocks), dim3(256), 0, s, a, n, f, k);
     return hipGetLastError();

@@ -214,7 +214,7 @@ class StateMachineRank:
         self.output_root = torch.full((cnt, R), NONE, dtype=torch.uint8, device=dev)
         self.faults = torch.zeros((cnt, R, max(1, max_faults)), dtype=torch.int16, device=dev)
         self.fault_count = torch.zeros((cnt, R), dtype=torch.int32, device=dev)
-        self.emitted = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.emitted = torch.zeros(2, dtype=torch.int32, device=dev)   # records, overflow flag
         # every sender's records of the previous round, [G][count][R][E][rec]
         self.inbox = torch.zeros((world, cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
         self.inbox_count = torch.zeros((world, cnt, R), dtype=torch.int32, device=dev)
@@ -260,10 +260,14 @@ class StateMachineRank:
         _check(_bind().hbrbc_sm_round(self.rb.coding.handle, ctypes.byref(a),
                                       ctypes.c_void_p(st.cuda_stream)))
 
-    def check_overflow(self):
-        if bool((self.out_count < 0).any()):   # bit 31: more than max_out records
+    def poll(self):
+        """Records emitted in the last round (one device-to-host read); raises
+        if a node emitted more than max_out (out_count bit 31)."""
+        e = self.emitted.cpu()
+        if int(e[1]):
             raise RuntimeError("state machine: a node emitted more than %d messages in a round"
                                % self.max_out)
+        return int(e[0])
 
     def exchange(self, ex, async_op=False):
         """All-gather of this round's records (the Ready / EchoHash / CanDecode
@@ -322,9 +326,7 @@ def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
     for r in range(max_rounds):
         for sm in ranks:
             sm.round(r)
-        for sm in ranks:
-            sm.check_overflow()
-        counts = [int(sm.emitted.item()) for sm in ranks]
+        counts = [sm.poll() for sm in ranks]
         for sm, c in zip(ranks, counts):
             sm.records += c
         emitted = sum(counts)

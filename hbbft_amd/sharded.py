@@ -314,6 +314,7 @@ class ShardedBroadcast:
                                    device=device, max_out=4, max_faults=4, ok=self.sm_ok,
                                    dec=self.sm_dec)
         self.sm_rounds = 0
+        self.sm_timing = None   # a list: (start, end) events of every run_state_machines
         self.own_cols = torch.tensor([j - rank * R for j in own] or [0], dtype=torch.int64,
                                      device=dev)
         self.own_rows = torch.tensor(own or [0], dtype=torch.int64, device=dev)
@@ -512,10 +513,17 @@ def run_state_machines(subs, ex):
     ShardedBroadcast objects of this rank, their messages all-gathered over
     `ex` each round; then every object's decided flags."""
     from .rbc_sim import run_rounds
+    ev = None
+    if subs[0].sm_timing is not None:   # events around all rounds (host gaps included)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     if ex.world > 1:
         rounds = run_rounds([sb.sm for sb in subs], ex)
     else:   # one rank: each object's nodes only talk to themselves
         rounds = max(run_rounds([sb.sm]) for sb in subs)
     for sb in subs:
         sb.finish()
+    if ev is not None:
+        ev[1].record()
+        subs[0].sm_timing.append(ev)
     return rounds

@@ -507,7 +507,8 @@ typedef struct hbrbc_sm_args {
     uint8_t *output_root;         /* [count][nodes]: decided root, NONE before */
     uint16_t *faults;             /* [count][nodes][max_faults] */
     uint32_t *fault_count;        /* [count][nodes] (may exceed max_faults) */
-    uint32_t *emitted;            /* += records emitted this round */
+    uint32_t *emitted;            /* [2]: [0] += records emitted this round, [1] |= 1 if a
+                                     node emitted more than max_out (out_count bit 31) */
 } hbrbc_sm_args;
 size_t hbrbc_sm_state_bytes(size_t n, size_t roots);
 /* One round for the hosted nodes of every instance (ctx gives n, f, k). */
