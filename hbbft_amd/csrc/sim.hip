@@ -94,6 +94,7 @@ struct Sm {
     // threads, so every state access of a wave is one coalesced request
     uint16_t *er;             // [n][sd]: echo entry | ready entry << 8
     uint32_t *cand;           // [C][W][sd]
+    uint32_t *full;           // [W][sd]: senders whose entry is a full Echo
     uint16_t *cnt;            // [3][C][sd]: Echo+EchoHash, full Echo, Ready counts
     uint32_t *flags;          // [sd]
     size_t sd;
@@ -111,6 +112,7 @@ struct Sm {
         w = (uint16_t)((w & 0xFFu) | (r << 8));
     }
     __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
+    __device__ uint32_t &FULL(int w) { return full[(size_t)w * sd]; }
     __device__ uint16_t &CE(uint32_t c) { return cnt[(size_t)c * sd]; }
     __device__ uint16_t &CF(uint32_t c) { return cnt[((size_t)C + c) * sd]; }
     __device__ uint16_t &CR(uint32_t c) { return cnt[((size_t)2 * C + c) * sd]; }
@@ -143,6 +145,29 @@ struct Sm {
         ++nout;
         r[0] = kind | (c << 8) | (j << 16) | (t << 24);
         return r;
+    }
+
+    // Recipient masks word by word (bit operations, not a loop over n: the
+    // lanes of a wave reach a send at different senders, so a per-node loop
+    // would run once per distinct trigger point).  lin(w, a, b): bits [a, b)
+    // of word w.
+    __device__ static uint32_t lin(int w, int a, int b) {
+        const int lo = a > 32 * w ? a : 32 * w, hi = b < 32 * w + 32 ? b : 32 * w + 32;
+        if (hi <= lo) return 0u;
+        const int len = hi - lo;
+        return (len >= 32 ? 0xFFFFFFFFu : ((1u << len) - 1u)) << (lo - 32 * w);
+    }
+    __device__ uint32_t all_but_me(int w) const {
+        return lin(w, 0, n) & ~((me >> 5) == w ? 1u << (me & 31) : 0u);
+    }
+    // right_nodes(me) (broadcast.rs:476-485): [me - f, me) on the circle
+    __device__ uint32_t right_mask(int w) const {
+        const int a0 = me - f;
+        return a0 >= 0 ? lin(w, a0, me) : (lin(w, 0, me) | lin(w, a0 + n, n));
+    }
+    template <class M>
+    __device__ void targets_w(uint32_t *r, M mask) {
+        for (int w = 0; w < W; ++w) r[1 + w] = mask(w);
     }
 
     // the recipient mask of record r: bit i set iff pred(i), each word built
@@ -188,7 +213,7 @@ struct Sm {
         if (!is_full(e) || root_of(e) != c) return;
         uint32_t *r = emit(K_ECHO, c, (uint32_t)me, tamper_of(e));
         if (!r) return;
-        targets(r, [&](int i) { return is_right_of(i, me) && !((CAND(c, i >> 5) >> (i & 31)) & 1u); });
+        targets_w(r, [&](int w) { return right_mask(w) & ~CAND(c, w); });
     }
 
     __device__ void handle_ready_core(int s, uint32_t c, bool may_send);
@@ -196,7 +221,7 @@ struct Sm {
     __device__ void send_ready(uint32_t c) {   // 513-522
         FLAGS() |= FL_READY_SENT;
         uint32_t *r = emit(K_READY, c);
-        if (r) targets(r, [&](int i) { return i != me; });
+        if (r) targets_w(r, [&](int w) { return all_but_me(w); });
         handle_ready_core(me, c, false);
     }
 
@@ -207,7 +232,7 @@ struct Sm {
     __device__ void send_can_decode(uint32_t c) {   // 488-510
         FLAGS() |= 1u << (FL_CAN_DECODE_SHIFT + c);
         uint32_t *r = emit(K_CAN_DECODE, c);
-        if (r) targets(r, [&](int i) { return i != me && !is_full(ECHO(i)); });
+        if (r) targets_w(r, [&](int w) { return all_but_me(w) & ~FULL(w); });
         handle_can_decode(me, c);
     }
 
@@ -228,6 +253,7 @@ struct Sm {
         if (!e) ++CE(c);   // a Hash of the same root was counted already
         ++CF(c);
         set_echo(s, enc_full(c, t));
+        FULL(s >> 5) |= 1u << (s & 31);
         if (!(FLAGS() & (1u << (FL_CAN_DECODE_SHIFT + c))) && CF(c) >= k) send_can_decode(c);
         if (!(FLAGS() & FL_READY_SENT) && CE(c) >= n - f) send_ready(c);
         if (FLAGS() & FL_READY_SENT) compute_output(c);
@@ -251,13 +277,13 @@ struct Sm {
     __device__ void send_echo_hash(uint32_t c) {   // 456-468
         FLAGS() |= FL_ECHO_HASH_SENT;
         uint32_t *r = emit(K_ECHO_HASH, c);
-        if (r) targets(r, [&](int i) { return is_right_of(i, me); });
+        if (r) targets_w(r, [&](int w) { return right_mask(w); });
         handle_echo_hash(me, c);
     }
 
     __device__ void send_echo_left(uint32_t c, uint32_t j, uint32_t t) {   // 413-425
         uint32_t *r = emit(K_ECHO, c, j, t);
-        if (r) targets(r, [&](int i) { return i != me && !is_right_of(i, me); });
+        if (r) targets_w(r, [&](int w) { return all_but_me(w) & ~right_mask(w); });
         handle_echo(me, c, j, t);
     }
 
@@ -366,13 +392,14 @@ __device__ void Sm::handle_ready_core(int s, uint32_t c, bool may_send) {   // 3
 
 // Byte offsets of the fields of an instance's state block holding `sd` nodes
 // as structures of arrays (include/hbrbc.h hbrbc_sm_state_bytes, per node:
-// er u16[n], cand u32[C][W], counters u16[3][C], flags u32).
+// er u16[n], cand u32[C][W], full u32[W], counters u16[3][C], flags u32).
 struct SmLayout {
-    size_t er, cand, cnt, flags;
+    size_t er, cand, full, cnt, flags;
     __device__ SmLayout(int n, int C, int W, size_t sd) {
         er = 0;
         cand = (2 * (size_t)n * sd + 3) & ~(size_t)3;
-        cnt = cand + 4 * (size_t)C * W * sd;
+        full = cand + 4 * (size_t)C * W * sd;
+        cnt = full + 4 * (size_t)W * sd;
         flags = (cnt + 6 * (size_t)C * sd + 3) & ~(size_t)3;
     }
 };
@@ -402,6 +429,7 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
     m.sd = sd;
     m.er = reinterpret_cast<uint16_t *>(st + L.er) + local;
     m.cand = reinterpret_cast<uint32_t *>(st + L.cand) + local;
+    m.full = reinterpret_cast<uint32_t *>(st + L.full) + local;
     m.cnt = reinterpret_cast<uint16_t *>(st + L.cnt) + local;
     m.flags = reinterpret_cast<uint32_t *>(st + L.flags) + local;
     m.pok = pok;
@@ -439,7 +467,7 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
                     // after the first delivered message (tests/broadcast.rs:73-97)
                     *m.flags |= FL_FAKE_DONE;
                     uint32_t *fr = m.emit_rec(K_FAKE, a.fake_root[inst], 0, 0);
-                    if (fr) m.targets(fr, [&](int i) { return i != me; });
+                    if (fr) m.targets_w(fr, [&](int w) { return m.all_but_me(w); });
                 }
             }
         }
