@@ -948,10 +948,35 @@ bool xor_streams() {   // measured no gain (cfg5 73.7 vs 73.2 GB/s, r3): off by 
     return e && !std::strcmp(e, "1");
 }
 
+// HBRBC_XOR_TILE=T (A/B): the programs of a split matrix walk the instances
+// T at a time (all programs over instances [i, i + T), then the next T), so
+// the T instances' input rows stay in the Infinity Cache between programs.
+size_t xor_tile() {
+    const char *e = getenv("HBRBC_XOR_TILE");
+    return e ? (size_t)atoll(e) : 0;
+}
+
 hipError_t launch_groups(hbrbc_ctx *c, const std::vector<hbrbc_ctx::SpecGroup> &gs, size_t first,
                          int rt, const XorArgs &x, size_t count, hipStream_t s) {
     const size_t ng = gs.size() - first;
     if (ng == 0) return hipSuccess;
+    const size_t tile = xor_tile();
+    if (ng > 1 && tile && count > tile) {
+        for (size_t i0 = 0; i0 < count; i0 += tile) {
+            XorArgs y = x;
+            y.base = x.base + i0 * x.inst_stride;
+            if (y.payloads) y.payloads = x.payloads + i0 * x.payload_stride;
+            if (y.pat) y.pat = x.pat + i0;
+            if (y.uf_payload) y.uf_payload = x.uf_payload + i0 * x.uf_stride;
+            if (y.uf_status) y.uf_status = x.uf_status + i0;
+            const size_t cnt = std::min(tile, count - i0);
+            for (size_t i = first; i < gs.size(); ++i) {
+                const hipError_t e = launch_xor_group(gs[i], false, rt, y, cnt, s);
+                if (e != hipSuccess) return e;
+            }
+        }
+        return hipSuccess;
+    }
     if (ng == 1 || !xor_streams()) {
         for (size_t i = first; i < gs.size(); ++i) {
             const hipError_t e = launch_xor_group(gs[i], false, rt, x, count, s);
