@@ -10,8 +10,9 @@ what a node emits in round t is delivered in round t + 1, handled in (sender,
 emission) order.  Every node's Echo / EchoHash / Ready / CanDecode state and
 counters live on the GPU; each round's messages (records of kind, root, proof
 index, tamper flag and an N-bit recipient mask) are all-gathered between the
-ranks (`StateMachineRank.exchange`), the Ready/EchoHash/CanDecode fan-out of
-SURVEY §5.
+ranks -- one all-gather per round for all of a rank's sub-batches, with their
+emitted counts and overflow flags (`_run_rounds_dist`) -- the
+Ready/EchoHash/CanDecode fan-out of SURVEY §5.
 
 Data plane.  Messages carry proofs by reference (root slot c, index j,
 tampered copy or not).  `data_plane` encodes each instance's codewords
@@ -317,39 +318,64 @@ def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
     topology for a loopback run (exchange None), or independent objects of
     this rank (e.g. pipelined sub-batches) with a DistExchange / SoloExchange
     `exchange`, whose world they share.  Returns the number of rounds."""
-    import torch.distributed as dist
     if fresh:
         for sm in ranks:
             sm.reset()
+    if exchange is not None and exchange.world > 1:
+        return _run_rounds_dist(ranks, exchange, max_rounds)
     loop = LoopbackExchange(ranks) if exchange is None and len(ranks) > 1 else None
-    world = exchange.world if exchange is not None else 1
     for r in range(max_rounds):
         for sm in ranks:
             sm.round(r)
         counts = [sm.poll() for sm in ranks]
         for sm, c in zip(ranks, counts):
             sm.records += c
-        emitted = sum(counts)
-        if world > 1:
-            t = torch.tensor([emitted], dtype=torch.int64, device=ranks[0].device)
-            if exchange.staged:
-                t = t.cpu()
-            dist.all_reduce(t, group=exchange.group)
-            emitted = int(t.item())
-        if emitted == 0:
+        if sum(counts) == 0:
             return r + 1
         if loop is not None:
             loop.gather()
-        elif world > 1:
-            hs = []
-            for sm in ranks:
-                hs += sm.exchange(exchange)
-            for h in hs:
-                if h is not None:
-                    h.wait()
         else:
             for sm in ranks:
                 sm.swap_local()
+    raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
+
+
+def _run_rounds_dist(ranks, ex, max_rounds):
+    """run_rounds over a process group: ONE all-gather per round carries every
+    sub-batch's records and counts plus each one's emitted count and overflow
+    flag (instead of an all-reduce and two all-gathers per sub-batch), and one
+    device-to-host read of the gathered tails decides termination."""
+    dev = ranks[0].device
+    parts = [(sm.out.numel(), sm.out_count.numel()) for sm in ranks]
+    k = len(ranks)
+    body = sum(a + b for a, b in parts)
+    send = torch.zeros(body + k + 1, dtype=torch.int32, device=dev)
+    recv = torch.empty((ex.world, body + k + 1), dtype=torch.int32, device=dev)
+    for r in range(max_rounds):
+        for sm in ranks:
+            sm.round(r)
+        off = 0
+        for sm, (a, b) in zip(ranks, parts):
+            send[off:off + a].copy_(sm.out.view(-1))
+            send[off + a:off + a + b].copy_(sm.out_count.view(-1))
+            off += a + b
+        tail = torch.stack([sm.emitted for sm in ranks])          # [k][2]
+        send[body:body + k].copy_(tail[:, 0])
+        send[body + k:].copy_(tail[:, 1].amax().view(1))
+        ex.all_gather(recv, send, name="sm_round")
+        t = recv[:, body:].cpu()                                   # [world][k + 1]
+        if int(t[:, k].max()):
+            raise RuntimeError("state machine: a node emitted more than %d messages in a round"
+                               % ranks[0].max_out)
+        for i, sm in enumerate(ranks):
+            sm.records += int(t[ex.rank, i])
+        if int(t[:, :k].sum()) == 0:
+            return r + 1
+        off = 0
+        for sm, (a, b) in zip(ranks, parts):
+            sm.inbox.view(ex.world, a).copy_(recv[:, off:off + a])
+            sm.inbox_count.view(ex.world, b).copy_(recv[:, off + a:off + a + b])
+            off += a + b
     raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
 
 

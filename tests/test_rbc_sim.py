@@ -213,7 +213,7 @@ def test_state_machine_matches_host_restatement(n, worlds):
 
 @pytest.mark.gpu
 def test_state_machine_counters_at_size():
-    """4096 honest N=64 instances and 4096 ProposeAdversary-with-drop
+    """128 honest N=64 instances and 128 ProposeAdversary-with-drop
     instances on 8 virtual ranks: every correct node decides the proposer's
     value (honest proposer), and the fault logs blame only faulty nodes."""
     from hbbft_amd.rbc_sim import simulate
@@ -235,3 +235,70 @@ def test_state_machine_counters_at_size():
             assert outs[(i, node)] == inst.values[0]
             assert all(b < f for b, _ in faults[(i, node)])
     assert rounds <= 8
+
+
+class _FakeSm:
+    """A StateMachineRank stand-in with the buffers _run_rounds_dist moves:
+    round r of rank g, sub-batch b writes records tagged (g, b, r) and emits
+    until round 2 (rank 1's sub-batch 1 until round 3)."""
+
+    def __init__(self, rank, world, b, count=3, R=2, E=2, rec=2):
+        self.rank, self.b, self.max_out = rank, b, E
+        self.device = torch.device("cpu")
+        self.out = torch.zeros((count, R, E, rec), dtype=torch.int32)
+        self.out_count = torch.zeros((count, R), dtype=torch.int32)
+        self.inbox = torch.zeros((world, count, R, E, rec), dtype=torch.int32)
+        self.inbox_count = torch.zeros((world, count, R), dtype=torch.int32)
+        self.emitted = torch.zeros(2, dtype=torch.int32)
+        self.records = 0
+        self.last = 2 if (rank, b) != (1, 1) else 3
+
+    def round(self, r):
+        active = r <= self.last
+        self.out.fill_(self.rank * 10000 + self.b * 1000 + r)
+        self.out_count.fill_(1 if active else 0)
+        self.emitted[0] = self.out_count.numel() if active else 0
+
+
+def _gloo_dist_rounds_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from hbbft_amd.rbc_sim import _run_rounds_dist
+    from hbbft_amd.sharded import DistExchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sms = [_FakeSm(rank, world, b) for b in range(2)]
+        rounds = _run_rounds_dist(sms, DistExchange(), 16)
+        good = rounds == 5   # the last emission (round 3) is delivered, round 4 is silent
+        for sm in sms:
+            # the inbox holds every rank's records of round 3 for this sub-batch
+            for g in range(world):
+                good &= bool((sm.inbox[g] == g * 10000 + sm.b * 1000 + 3).all())
+                good &= bool((sm.inbox_count[g] == (1 if (g, sm.b) == (1, 1) else 0)).all())
+            good &= sm.records == sm.out_count.numel() * (sm.last + 1)
+        q.put((rank, "ok" if good else "mismatch rounds=%d" % rounds))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_fused_round_exchange():
+    """_run_rounds_dist (one all-gather per round for all sub-batches, emitted
+    counts and overflow flags in the tail) on a gloo world of 2: termination
+    round, every rank's records in every sub-batch's inbox, record counts."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_gloo_dist_rounds_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: "ok", 1: "ok"}, res
