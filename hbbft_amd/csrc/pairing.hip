@@ -15,7 +15,7 @@
 //
 // MI355X layout.  One lane owns one Miller loop (kernel 1) or one final
 // exponentiation (kernel 2): the arithmetic is serial 381-bit Montgomery
-// products on 12 x 32-bit limbs (v_mad_u64_u32 chains), so a lane-per-pairing
+// products (12 x 32-bit limbs at rest, 14 x 29-bit limbs inside fp_mul), so a lane-per-pairing
 // mapping keeps every limb in VGPRs with no cross-lane traffic.  The Miller
 // values travel between the kernels in a limb-major workspace
 // ([144 words][pairings]), so every store and load is one coalesced dword per
@@ -124,54 +124,78 @@ DEV void fp_neg(Fp &r, const Fp &a) {
     fp_sub(r, z, a);
 }
 
-// One Montgomery step of CIOS: t <- (t + m p) / 2^32 with m = t0 * (-p^-1).
-// The 12 products m*p_j + t_j are independent (v_mad_u64_u32 with the limb as
-// addend); their high halves ride one add-with-carry chain.
-DEV void mont_step(uint32_t (&t)[NL + 1]) {
-    const uint32_t m = t[0] * kInv32;
-    uint64_t q[NL];
+// Montgomery product a*b*2^-406 mod p (R = 2^406, bls_consts.hpp), product
+// scanning over 14 limbs of 29 bits: column k of a*b + M*p is a sum of at
+// most 28 products < 2^58 plus the carry, so it accumulates in a 64-bit value
+// fed straight by v_mad_u64_u32 (the accumulator is the 64-bit addend: no
+// zero-extending moves, no carry chains, no carry-flag hazards); each of the
+// first 14 columns fixes one 29-bit Montgomery digit m_k.  Two accumulators per
+// column (even / odd i) halve the dependent chains.  561 VALU per product
+// against 1078 for 32-bit-limb CIOS (288 mads + 248 moves + 264 add-with-carry
+// + 205 hazard nops), DESIGN.md §6e.  Inputs < p in 12 x 32-bit limbs; the
+// result < 2p is reduced once.
+constexpr uint32_t kM29 = (1u << 29) - 1;
+
+DEV void fp_to29(uint32_t (&o)[14], const uint32_t (&w)[NL]) {
 #pragma unroll
-    for (int j = 0; j < NL; ++j) q[j] = (uint64_t)m * kP[j] + t[j];
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 1; j < NL; ++j) t[j - 1] = addc((uint32_t)q[j], (uint32_t)(q[j - 1] >> 32), c, &c);
-    t[NL - 1] = addc(t[NL], (uint32_t)(q[NL - 1] >> 32), c, &c);
-    t[NL] = c;
+    for (int i = 0; i < 14; ++i) {
+        const int bit = 29 * i, q = bit >> 5, s = bit & 31;
+        const uint32_t lo = w[q], hi = (q + 1 < NL) ? w[q + 1] : 0u;
+        o[i] = (s ? __builtin_amdgcn_alignbit(hi, lo, s) : lo) & kM29;
+    }
 }
 
-// Montgomery product a*b*2^-384 mod p, CIOS over 32-bit limbs (p < 2^381, so
-// the running value stays below 2p and one extra word holds every carry).
-// Per row: 12 independent a_j*b_i + t_j products, one carry chain over their
-// high halves, one Montgomery step -- two VALU per limb product.
 DEV void fp_mul(Fp &r, const Fp &a, const Fp &b) {
-    uint32_t t[NL + 1];
-    {
-        uint64_t p[NL];
+    uint32_t x[14], y[14], m[14], o[14];
+    fp_to29(x, a.l);
+    fp_to29(y, b.l);
+    uint64_t acc = 0;
 #pragma unroll
-        for (int j = 0; j < NL; ++j) p[j] = (uint64_t)a.l[j] * b.l[0];
-        uint32_t c = 0;
-        t[0] = (uint32_t)p[0];
+    for (int k = 0; k < 14; ++k) {
+        uint64_t e = acc, f = 0;
 #pragma unroll
-        for (int j = 1; j < NL; ++j) t[j] = addc((uint32_t)p[j], (uint32_t)(p[j - 1] >> 32), c, &c);
-        t[NL] = (uint32_t)(p[NL - 1] >> 32) + c;
-        mont_step(t);
+        for (int i = 0; i <= k; ++i) {
+            if (i & 1) f += (uint64_t)x[i] * y[k - i];
+            else e += (uint64_t)x[i] * y[k - i];
+        }
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+            if (i & 1) f += (uint64_t)m[i] * kP29[k - i];
+            else e += (uint64_t)m[i] * kP29[k - i];
+        }
+        acc = e + f;
+        m[k] = ((uint32_t)acc * kPinv29) & kM29;
+        acc += (uint64_t)m[k] * kP29[0];   // low 29 bits become 0
+        acc >>= 29;
     }
 #pragma unroll
-    for (int i = 1; i < NL; ++i) {
-        uint64_t p[NL];
+    for (int k = 14; k < 27; ++k) {
+        uint64_t e = acc, f = 0;
 #pragma unroll
-        for (int j = 0; j < NL; ++j) p[j] = (uint64_t)a.l[j] * b.l[i] + t[j];
-        uint32_t c = 0;
-        t[0] = (uint32_t)p[0];
+        for (int i = k - 13; i < 14; ++i) {
+            if (i & 1) f += (uint64_t)x[i] * y[k - i];
+            else e += (uint64_t)x[i] * y[k - i];
+        }
 #pragma unroll
-        for (int j = 1; j < NL; ++j) t[j] = addc((uint32_t)p[j], (uint32_t)(p[j - 1] >> 32), c, &c);
-        t[NL] = t[NL] + (uint32_t)(p[NL - 1] >> 32) + c;
-        mont_step(t);
+        for (int i = k - 13; i < 14; ++i) {
+            if (i & 1) f += (uint64_t)m[i] * kP29[k - i];
+            else e += (uint64_t)m[i] * kP29[k - i];
+        }
+        acc = e + f;
+        o[k - 14] = (uint32_t)acc & kM29;
+        acc >>= 29;
     }
-    uint32_t u[NL];
+    o[13] = (uint32_t)acc;   // < 2^5: the result is below 2p < 2^382
+    uint32_t t[NL];
 #pragma unroll
-    for (int i = 0; i < NL; ++i) u[i] = t[i];
-    fp_reduce_once(r, u);
+    for (int j = 0; j < NL; ++j) {   // back to 12 x 32-bit limbs
+        const int bit = 32 * j, i = bit / 29, s = bit % 29;
+        uint32_t v = o[i] >> s;
+        if (i + 1 < 14) v |= o[i + 1] << (29 - s);
+        if (s > 26 && i + 2 < 14) v |= o[i + 2] << (58 - s);
+        t[j] = v;
+    }
+    fp_reduce_once(r, t);
 }
 
 DEV void fp_sqr(Fp &r, const Fp &a) { fp_mul(r, a, a); }
@@ -840,12 +864,20 @@ DEV void load_f12(Fp12 &f, const uint32_t *ws, size_t n, size_t i) {
 }
 
 constexpr int kPairBlock = 64;
+// waves per SIMD of every pairing kernel (512 / HB_PAIR_WPE VGPRs per lane).
+// The 29-bit-limb product holds x, y, m and the output digits (56 VGPRs) on
+// top of the tower operands: at 4 waves (128 VGPRs) the kernels spilled
+// (1.02 M checks/s), at 2 waves (256 VGPRs) 1.57 M, at 1 wave 1.53 M (r3,
+// tools/gpu_f4_wpe.sh; -DHB_PAIR_WPE=1|4 builds the A/B variants)
+#ifndef HB_PAIR_WPE
+#define HB_PAIR_WPE 2
+#endif
 
 // Kernel 1: one Miller loop per lane.  Pairing i takes G1 point g1[i] and G2
 // point g2[i]; with `negate_odd`, odd pairings negate their G1 point (the
 // c of a check a,b == c,d sits at pairing 2i+1).  status[i] gets the point
 // status (max of the two); an infinity or invalid input leaves f = 1.
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void miller_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void miller_kernel(
     const uint8_t *__restrict__ g1, size_t g1_stride, const uint8_t *__restrict__ g2,
     size_t g2_stride, size_t n, int pair_inputs, uint32_t *__restrict__ ws,
     uint8_t *__restrict__ status) {
@@ -884,7 +916,7 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4
 // at rows 2i, 2i+1): the two Miller loops of f_a,b * f_-c,d share one
 // squaring of f per step (a multi-Miller loop; the product is what the final
 // exponentiation needs).  An infinity drops its pairing's lines (factor 1).
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void miller2_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void miller2_kernel(
     const uint8_t *__restrict__ g1, const uint8_t *__restrict__ g2, size_t count,
     uint32_t *__restrict__ ws, uint8_t *__restrict__ status) {
     const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
@@ -960,7 +992,7 @@ DEV void load_line(const uint32_t *src, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
 
 // One lane per G2 point: its 68 lines, and its status (0 ok, 1 infinity,
 // 2 invalid) at pst[q].
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void g2_prepare_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void g2_prepare_kernel(
     const uint8_t *__restrict__ g2, size_t count, uint32_t *__restrict__ prep,
     uint8_t *__restrict__ pst) {
     const size_t q = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
@@ -998,7 +1030,7 @@ NOINL void apply_prepared(Fp12 &f, const uint32_t *line, const Fp &xp, const Fp 
 // id[i] of the table): g1 holds a, c at rows 2i, 2i+1.  Lanes of a wave
 // checking against the same points read the same lines (one cache line
 // serves the wave).
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void miller_prepared_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void miller_prepared_kernel(
     const uint8_t *__restrict__ g1, const uint32_t *__restrict__ prep,
     const uint8_t *__restrict__ pst, const uint32_t *__restrict__ ib,
     const uint32_t *__restrict__ id, size_t points, size_t count, uint32_t *__restrict__ ws,
@@ -1090,7 +1122,7 @@ DEV void store_be48(uint8_t *dst, const Fp &a) {
 // (1: a pairing, 2: a check) are multiplied first.  gt_out (if set) gets the
 // 576-byte GT value; ok_out (if set) gets 1 if the value is 1 (the check
 // holds), 0 if not, 2 if an input point was invalid.
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void final_exp_kernel(
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void final_exp_kernel(
     const uint32_t *__restrict__ ws, size_t n_miller, size_t n_out, int per_out,
     const uint8_t *__restrict__ status, uint8_t *__restrict__ gt_out,
     uint8_t *__restrict__ ok_out) {
