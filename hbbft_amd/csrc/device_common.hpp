@@ -122,6 +122,9 @@ __device__ __forceinline__ void keccak_f1600(uint32_t (&L)[25], uint32_t (&H)[25
 // separate instantiation: compiled into the same kernel as the 8-byte path
 // its two block buffers set the kernel's VGPR count (152 -> 3 waves/SIMD for
 // every grid, 130 without it).
+#ifndef HB_SPONGE_PF
+#define HB_SPONGE_PF 1
+#endif
 template <bool V16 = false>
 __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint32_t len,
                                              uint32_t (&out)[8]) {
@@ -198,6 +201,7 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
     // permuted, so the sponge never waits on memory between permutations
     // (+34 VGPRs; the sponge kernels run at 4 waves/SIMD either way).
     if (nfull) {
+#if HB_SPONGE_PF
         uint2 nx[17];
 #pragma unroll
         for (int w = 0; w < 17; ++w) nx[w] = q[w];
@@ -214,6 +218,20 @@ __device__ __forceinline__ void sha3_256_row(const uint8_t *__restrict__ p, uint
             }
             keccak_f1600(L, H);
         }
+#else
+        // no software pipeline: 34 fewer VGPRs, more waves per SIMD hide
+        // the load latency instead (HB_SPONGE_PF=0, A/B)
+        for (uint32_t t = 0; t < nfull; ++t) {
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                const uint2 v = q[w];
+                L[w] ^= v.x;
+                H[w] ^= v.y;
+            }
+            q += 17;
+            keccak_f1600(L, H);
+        }
+#endif
     }
     // last (partial) block + pad10*1 with the SHA3 domain byte 0x06
     const int r = (int)(len - nfull * 136u);

@@ -381,7 +381,10 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
 // (slens != nullptr: ragged batch, instance i's shards are slens[i] bytes.)
 // Sponge kernels: at most 128 VGPRs (4 waves/SIMD, the residency the
 // Keccak ceiling was measured at); V16 = few-sponge grids (16-byte loads).
-#define HB_SPONGE_ATTR __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(V16 ? 1 : 4)))
+#ifndef HB_SPONGE_WPE
+#define HB_SPONGE_WPE 4   // waves/SIMD of the 8-byte-load sponge kernels (A/B: -DHB_SPONGE_WPE)
+#endif
+#define HB_SPONGE_ATTR __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(V16 ? 1 : HB_SPONGE_WPE)))
 template <bool V16>
 __global__ HB_SPONGE_ATTR void leaf_hash_kernel(
     const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
