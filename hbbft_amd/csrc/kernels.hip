@@ -213,24 +213,26 @@ __device__ __forceinline__ void bs_transpose(uint32_t (&w)[8]) {
 }
 
 // Fused unframe (decode_from_shards, broadcast.rs:590-598): 16 bytes of data
-// row `row` at byte `pos` are payload bytes row*S + pos - 4 .. +15 (S % 4 == 0,
-// so every destination is dword-aligned; unaligned-access mode stores 16 B at
-// once).  Bytes of the row padding (pos >= S) and the 4-byte length prefix are
-// not payload.  The fixup after the root check zero-fills past the length.
-typedef uint32_t hb_u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+// row `row` at byte `pos` are payload bytes row*S + pos - 4 .. +15.  Inside
+// the row one 16-byte store at any byte alignment (the AMDGPU ABI runs global
+// memory in unaligned mode, and hipcc emits global_store_dwordx4 for it); the
+// 4-byte length prefix (row 0) and the row's last chunk, whose bytes past S
+// belong to the next row's writer, go byte by byte.  Bytes of the row padding
+// (pos >= S) are not payload.  The fixup after the root check zero-fills past
+// the length.
+typedef uint32_t hb_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ void unframe_put(uint8_t *pb, uint32_t S, uint32_t row, uint32_t pos,
                                             uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     if (pos >= S) return;
     const int64_t dst = (int64_t)row * S + pos - 4;
     if (dst >= 0 && pos + 16 <= S) {
-        *reinterpret_cast<hb_u32x4_a4 *>(pb + dst) = (hb_u32x4_a4){a, b, c, d};
+        *reinterpret_cast<hb_u32x4_a1 *>(pb + dst) = (hb_u32x4_a1){a, b, c, d};
         return;
     }
     const uint32_t w[4] = {a, b, c, d};
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (pos + 4 * q < S && dst + 4 * q >= 0)
-            *reinterpret_cast<uint32_t *>(pb + dst + 4 * q) = w[q];
+    for (int q = 0; q < 16; ++q)
+        if (pos + q < S && dst + q >= 0) pb[dst + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
 }
 
 template <int RT, int MODE>
