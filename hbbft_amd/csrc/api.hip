@@ -479,10 +479,9 @@ hipError_t launch_groups(hbrbc_ctx *c, const std::vector<hbrbc_ctx::SpecGroup> &
 // Fused unframe (decode paths): the generic reconstruct kernel writes the
 // payload bytes of the data rows it reads or rebuilds, so unframe's re-read of
 // k*S bytes per instance disappears (decode_check + a zero-fill fixup remain).
-// The generic kernel fuses at any S (byte-aligned 16-byte stores, round 3;
-// cfg4 S % 4 = 2); the pattern-specialised decoders' _uf variants (v17 code
-// objects) need S % 4 == 0 (dword-aligned destinations), so with one of them
-// and another S the call unframes separately (run_reconstruct).
+// Any S (byte-aligned 16-byte stores, round 3; cfg4 S % 4 = 2, cfg5 S odd),
+// in the generic kernel and in the pattern-specialised decoders' _uf
+// variants (v20 code objects).
 // HBRBC_UNFRAME_FUSED=0 keeps the separate unframe (A/B).
 bool unframe_fusable(const hbrbc_ctx *c, size_t shard_len, size_t payload_stride) {
     const char *e = getenv("HBRBC_UNFRAME_FUSED");
@@ -576,8 +575,7 @@ int run_reconstruct(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMa
     if (c->m == 0) return HBRBC_OK;  // Coding::Trivial: nothing to rebuild
     StageTimer t(c, HBRBC_STAGE_RECONSTRUCT, s);
     // fusing with a specialised decoder needs its _uf variant
-    if (spec && uf_payload && (shard_len % 4 || !uf_decoder(c, ds->second, code_rb(rows))))
-        uf_payload = nullptr;
+    if (spec && uf_payload && !uf_decoder(c, ds->second, code_rb(rows))) uf_payload = nullptr;
     if (spec) {
         XorArgs x{};
         x.base = shards;
@@ -648,7 +646,7 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v19.co";   // v19: plain decoders + _uf variants
+           "_v20.co";   // v20: _uf variants store the payload at any byte alignment
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
@@ -2152,8 +2150,7 @@ int hbrbc_unframe_fused(const hbrbc_ctx *c, size_t shard_len, size_t payload_str
     const auto ds = c->dec_spec.find(code_rb(rows));
     const bool spec = ds != c->dec_spec.end() && !ds->second.groups.empty();
     // with a specialised decoder, its _uf variant (untried: assumed loadable)
-    return unframe_fusable(c, shard_len, payload_stride) &&
-                   (!spec || (shard_len % 4 == 0 && ds->second.uf_state >= 0))
+    return unframe_fusable(c, shard_len, payload_stride) && (!spec || ds->second.uf_state >= 0)
                ? 1 : 0;
 }
 
