@@ -83,6 +83,11 @@ __device__ __forceinline__ bool is_hash(uint32_t e) { return e & 0x10u; }
 __device__ __forceinline__ uint32_t root_of(uint32_t e) { return e & 7u; }
 __device__ __forceinline__ uint32_t tamper_of(uint32_t e) { return (e >> 3) & 1u; }
 
+// ONE: a single codeword slot (roots == 1, the validator-sharded runs): the
+// node's Echo / full-Echo / Ready counters and its flags live in registers
+// for the round (the handlers are chains of dependent read-modify-writes of
+// them), written back at the end.
+template <bool ONE>
 struct Sm {
     const hbrbc_sm_args &a;
     int n, f, k, W, C, rec;   // rec: uint32 words per message record (1 + W)
@@ -113,10 +118,40 @@ struct Sm {
     }
     __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
     __device__ uint32_t &FULL(int w) { return full[(size_t)w * sd]; }
-    __device__ uint16_t &CE(uint32_t c) { return cnt[(size_t)c * sd]; }
-    __device__ uint16_t &CF(uint32_t c) { return cnt[((size_t)C + c) * sd]; }
-    __device__ uint16_t &CR(uint32_t c) { return cnt[((size_t)2 * C + c) * sd]; }
-    __device__ uint32_t &FLAGS() { return *flags; }
+    uint16_t r_ce = 0, r_cf = 0, r_cr = 0;
+    uint32_t r_flags = 0;
+    __device__ uint16_t &CE(uint32_t c) {
+        if constexpr (ONE) return r_ce;
+        else return cnt[(size_t)c * sd];
+    }
+    __device__ uint16_t &CF(uint32_t c) {
+        if constexpr (ONE) return r_cf;
+        else return cnt[((size_t)C + c) * sd];
+    }
+    __device__ uint16_t &CR(uint32_t c) {
+        if constexpr (ONE) return r_cr;
+        else return cnt[((size_t)2 * C + c) * sd];
+    }
+    __device__ uint32_t &FLAGS() {
+        if constexpr (ONE) return r_flags;
+        else return *flags;
+    }
+    __device__ void cache_in() {
+        if constexpr (ONE) {
+            r_ce = cnt[0];
+            r_cf = cnt[sd];
+            r_cr = cnt[2 * sd];
+            r_flags = *flags;
+        }
+    }
+    __device__ void cache_out() {
+        if constexpr (ONE) {
+            cnt[0] = r_ce;
+            cnt[sd] = r_cf;
+            cnt[2 * sd] = r_cr;
+            *flags = r_flags;
+        }
+    }
     uint32_t *out;            // [max_out][rec]
     uint32_t nout;
     bool overflow;
@@ -375,7 +410,8 @@ struct Sm {
     }
 };
 
-__device__ void Sm::handle_ready_core(int s, uint32_t c, bool may_send) {   // 378-410
+template <bool ONE>
+__device__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {   // 378-410
     const uint32_t old = READY(s);
     if (old) {
         if (old - 1 != c) fault(s, F_MULTIPLE_READYS);
@@ -407,7 +443,7 @@ struct SmLayout {
 // Handles one node's inbox of the round (or, in round 0, the proposer's
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
 // `inc(s)` sender s's record count, `recs(s)` its records.
-template <class InCount, class Recs>
+template <bool ONE, class InCount, class Recs>
 __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
                         InCount inc, Recs recs) {
@@ -415,7 +451,7 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
     const int W = (n + 31) / 32, C = (int)a.roots;
     const size_t sd = a.nodes;
     const SmLayout L(n, C, W, sd);
-    Sm m{a};
+    Sm<ONE> m{a};
     m.n = n;
     m.f = f;
     m.k = k;
@@ -439,13 +475,14 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
     m.overflow = false;
     m.faults = a.faults + g * (size_t)a.max_faults;
     m.nfault = a.fault_count[g];
+    m.cache_in();
     if (a.round == 0) {
         // the proposer's broadcast() (broadcast.rs:123-137, 170-225): its input
         // step goes out unfiltered (VirtualNet::send_input; only deliveries to
         // faulty nodes pass the adversary)
         m.drop = false;
-        if (me == m.proposer && !(*m.flags & FL_VALUE_SENT)) {
-            *m.flags |= FL_VALUE_SENT;
+        if (me == m.proposer && !(m.FLAGS() & FL_VALUE_SENT)) {
+            m.FLAGS() |= FL_VALUE_SENT;
             uint32_t *r = m.emit_rec(K_VALUE, kNone, 0, 0);
             if (r)
                 m.targets(r, [&](int i) { return i != me && a.value_root[inst * n + i] != kNone; });
@@ -463,15 +500,16 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
                 const uint32_t *r = rs + (size_t)e * (1 + W);
                 if (!m.bit(r + 1, me)) continue;
                 m.deliver(s, r);
-                if (faker && !(*m.flags & FL_FAKE_DONE)) {
+                if (faker && !(m.FLAGS() & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
-                    *m.flags |= FL_FAKE_DONE;
+                    m.FLAGS() |= FL_FAKE_DONE;
                     uint32_t *fr = m.emit_rec(K_FAKE, a.fake_root[inst], 0, 0);
                     if (fr) m.targets_w(fr, [&](int w) { return m.all_but_me(w); });
                 }
             }
         }
     }
+    m.cache_out();
     a.out_count[g] = m.nout | (m.overflow ? 0x80000000u : 0u);
     a.fault_count[g] = m.nfault;
     if (m.nout) atomicAdd(a.emitted, m.nout);
@@ -486,6 +524,7 @@ __device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t ins
 // Round kernel, global form: one thread per (instance, hosted node), state,
 // records and outcomes read where they lie.  For blocks whose staged copy
 // does not fit the LDS budget (sm_plan).
+template <bool ONE>
 __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, int f, int k) {
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (g >= a.count * a.nodes) return;
@@ -494,7 +533,7 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     if ((int)a.node_lo + local >= n) return;
     const size_t MR = (size_t)a.max_out * ((n + 31) / 32 + 1);
     uint8_t *st = a.state + inst * a.nodes * sm_state_bytes(n, a.roots);
-    sm_node(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
+    sm_node<ONE>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
             a.decode_ok + inst * a.roots,
             [&](int s) {
                 const uint32_t c = a.in_count[sm_in_block(a, inst, s)] & 0x7FFFFFFFu;
@@ -510,6 +549,7 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
 // dependent read-modify-write chains (handle_echo: entry, Echo count, full
 // count, flags, outcome, ...) then cost LDS latency instead of an L2 round
 // trip each.  The state goes back at the end.
+template <bool ONE>
 __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
                                                              int k, int ipb) {
     extern __shared__ uint4 sm_lds4[];
@@ -555,7 +595,7 @@ __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, i
         const size_t inst = inst0 + li;
         const uint32_t *cb = lcnt + (size_t)li * n;
         const uint32_t *rb = lrec + (size_t)li * n * MR;
-        sm_node(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
+        sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
                 lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
                 [&](int s) { return cb[s]; }, [&](int s) { return rb + (size_t)s * MR; });
     }
@@ -585,12 +625,21 @@ hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStrea
     while (ipb > 1 && sm_lds_bytes(a, n, ipb) > 65536) --ipb;
     if (staged_ok && sm_lds_bytes(a, n, ipb) <= 65536) {
         const unsigned blocks = (unsigned)((a.count + ipb - 1) / ipb);
-        hipLaunchKernelGGL(sm_round_staged_kernel, dim3(blocks), dim3((unsigned)(ipb * a.nodes)),
-                           sm_lds_bytes(a, n, ipb), s, a, n, f, k, ipb);
+        if (a.roots == 1)
+            hipLaunchKernelGGL(sm_round_staged_kernel<true>, dim3(blocks),
+                               dim3((unsigned)(ipb * a.nodes)), sm_lds_bytes(a, n, ipb), s, a, n,
+                               f, k, ipb);
+        else
+            hipLaunchKernelGGL(sm_round_staged_kernel<false>, dim3(blocks),
+                               dim3((unsigned)(ipb * a.nodes)), sm_lds_bytes(a, n, ipb), s, a, n,
+                               f, k, ipb);
         return hipGetLastError();
     }
     const unsigned blocks = (unsigned)((threads + 255) / 256);
-    hipLaunchKernelGGL(sm_round_kernel, dim3(blocks), dim3(256), 0, s, a, n, f, k);
+    if (a.roots == 1)
+        hipLaunchKernelGGL(sm_round_kernel<true>, dim3(blocks), dim3(256), 0, s, a, n, f, k);
+    else
+        hipLaunchKernelGGL(sm_round_kernel<false>, dim3(blocks), dim3(256), 0, s, a, n, f, k);
     return hipGetLastError();
 }
 
