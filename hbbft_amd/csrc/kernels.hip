@@ -798,6 +798,7 @@ __global__ __launch_bounds__(kBlock) void pattern_lookup_kernel(
 // M[missing] * inv(M[valid]) (missing data rows are rows of the inverse;
 // missing parity rows equal rse's parity-from-rebuilt-data by linearity over
 // GF(2^8)), as coefficient bytes [pass][k][16] for gf_bitslice_kernel.
+// LDS: 1600 B of tables and lists + d x 2d + d x (k - d) <= 1600 + 3 k^2.
 __global__ __launch_bounds__(1024) void decode_matrix_kernel(
     int n, int k, int rt, const uint8_t *__restrict__ matrix, const uint8_t *__restrict__ present,
     PatternCache c, int *__restrict__ pat, const uint8_t *__restrict__ own) {
@@ -807,8 +808,8 @@ __global__ __launch_bounds__(1024) void decode_matrix_kernel(
     uint8_t *valid = smem + 768;       // 256
     uint8_t *missing = smem + 1024;    // 256
     uint8_t *fac = smem + 1280;        // 256
-    int *meta = reinterpret_cast<int *>(smem + 1536);  // [0]=npresent [1]=nmiss [2]=pivot [3]=inv [4]=singular [5]=slot
-    uint8_t *aug = smem + 1600;        // k x 2k
+    int *meta = reinterpret_cast<int *>(smem + 1536);  // [0]=npresent [1]=nmiss [2]=pivot [3]=inv [4]=singular [5]=slot [6]=missing data rows
+    uint8_t *aug = smem + 1600;        // d x 2d [A | I], then d x (k - d) Ainv B
     const int m = n - k;
     const size_t inst = blockIdx.x;
     const int tid = threadIdx.x;
@@ -840,9 +841,12 @@ __global__ __launch_bounds__(1024) void decode_matrix_kernel(
                 missing[nm++] = (uint8_t)i;
             }
         }
+        int dm = 0;
+        while (dm < nm && missing[dm] < k) ++dm;   // missing is ascending: data rows first
         meta[0] = np;
         meta[1] = nm;
         meta[4] = 0;
+        meta[6] = dm;
     }
     __syncthreads();
     const int np = meta[0], nm = meta[1];
@@ -853,75 +857,101 @@ __global__ __launch_bounds__(1024) void decode_matrix_kernel(
         }
         return;
     }
-    const int w2 = 2 * k;
-    for (int e = tid; e < k * w2; e += nt) {
-        const int r = e / w2, col = e - r * w2;
-        aug[e] = (col < k) ? matrix[(size_t)valid[r] * k + col] : (uint8_t)((col - k) == r);
-    }
-    __syncthreads();
-    for (int col0 = 0; col0 < k; ++col0) {
-        if (tid < 64) {   // pivot: first nonzero row at or below col0, by ballot over 64 rows
-            int p = -1;
-            for (int r0 = col0; r0 < k && p < 0; r0 += 64) {
-                const int r = r0 + tid;
-                const unsigned long long bal = __ballot(r < k && aug[r * w2 + col0] != 0);
-                if (bal) p = r0 + __ffsll((long long)bal) - 1;
-            }
-            if (tid == 0) meta[2] = p;
-        }
-        if (tid == 0) {
-            const int p = meta[2];
-            if (p < 0)
-                meta[4] = 1;
-            else
-                meta[3] = gf_inv_lds(exp_t, log_t, aug[p * w2 + col0]);
-        }
-        __syncthreads();
-        if (meta[4]) {
-            if (tid == 0) {
-                c.nout[slot] = 0;
-                c.status[slot] = 64;  // SingularMatrix (impossible for an MDS code)
-            }
-            return;
-        }
-        const int p = meta[2];
-        const uint8_t inv = (uint8_t)meta[3];
-        if (p != col0) {
-            for (int col = tid; col < w2; col += nt) {
-                uint8_t t = aug[col0 * w2 + col];
-                aug[col0 * w2 + col] = aug[p * w2 + col];
-                aug[p * w2 + col] = t;
-            }
-        }
-        __syncthreads();
-        for (int col = tid; col < w2; col += nt)
-            aug[col0 * w2 + col] = gf_mul_lds(exp_t, log_t, inv, aug[col0 * w2 + col]);
-        __syncthreads();
-        for (int r = tid; r < k; r += nt) fac[r] = (r == col0) ? 0 : aug[r * w2 + col0];
-        __syncthreads();
-        for (int e = tid; e < k * w2; e += nt) {
+    // rse's decode rows, structured: rows 0..k-1 of the encoding matrix are the
+    // identity, and first-k-present gives valid = D ++ P' (the k - d present
+    // data rows, then the first d present parity rows), so the d missing data
+    // rows solve A x_miss = y_P' + B y_D with A = M[P'][miss], B = M[P'][D]:
+    // x_miss = Ainv y_P' + (Ainv B) y_D.  Only the d x d matrix A is inverted
+    // (Gauss-Jordan in LDS, d ~ f k / n: 7 at cfg3 instead of 22); the rows are
+    // those of inv(M[valid]) (unique), and a missing parity row p is M[p] times
+    // them.  (Round 2 inverted all of M[valid], k x 2k.)
+    const int d = meta[6], kd = k - d, w2 = 2 * d;
+    uint8_t *X = aug + (size_t)d * w2;   // d x kd: Ainv B
+    if (d > 0) {
+        for (int e = tid; e < d * w2; e += nt) {
             const int r = e / w2, col = e - r * w2;
-            const uint8_t f = fac[r];
-            if (f) aug[e] ^= gf_mul_lds(exp_t, log_t, f, aug[col0 * w2 + col]);
+            aug[e] = (col < d) ? matrix[(size_t)valid[kd + r] * k + missing[col]]
+                               : (uint8_t)((col - d) == r);
+        }
+        __syncthreads();
+        for (int col0 = 0; col0 < d; ++col0) {
+            if (tid < 64) {   // pivot: first nonzero row at or below col0, by ballot
+                int p = -1;
+                for (int r0 = col0; r0 < d && p < 0; r0 += 64) {
+                    const int r = r0 + tid;
+                    const unsigned long long bal = __ballot(r < d && aug[r * w2 + col0] != 0);
+                    if (bal) p = r0 + __ffsll((long long)bal) - 1;
+                }
+                if (tid == 0) meta[2] = p;
+            }
+            if (tid == 0) {
+                const int p = meta[2];
+                if (p < 0)
+                    meta[4] = 1;
+                else
+                    meta[3] = gf_inv_lds(exp_t, log_t, aug[p * w2 + col0]);
+            }
+            __syncthreads();
+            if (meta[4]) {
+                if (tid == 0) {
+                    c.nout[slot] = 0;
+                    c.status[slot] = 64;  // SingularMatrix (impossible for an MDS code)
+                }
+                return;
+            }
+            const int p = meta[2];
+            const uint8_t inv = (uint8_t)meta[3];
+            if (p != col0) {
+                for (int col = tid; col < w2; col += nt) {
+                    uint8_t t = aug[col0 * w2 + col];
+                    aug[col0 * w2 + col] = aug[p * w2 + col];
+                    aug[p * w2 + col] = t;
+                }
+            }
+            __syncthreads();
+            for (int col = tid; col < w2; col += nt)
+                aug[col0 * w2 + col] = gf_mul_lds(exp_t, log_t, inv, aug[col0 * w2 + col]);
+            __syncthreads();
+            for (int r = tid; r < d; r += nt) fac[r] = (r == col0) ? 0 : aug[r * w2 + col0];
+            __syncthreads();
+            for (int e = tid; e < d * w2; e += nt) {
+                const int r = e / w2, col = e - r * w2;
+                const uint8_t f = fac[r];
+                if (f) aug[e] ^= gf_mul_lds(exp_t, log_t, f, aug[col0 * w2 + col]);
+            }
+            __syncthreads();
+        }
+        for (int e = tid; e < d * kd; e += nt) {   // X = Ainv B
+            const int i = e / kd, cc = e - i * kd;
+            uint8_t acc = 0;
+            for (int r = 0; r < d; ++r)
+                acc ^= gf_mul_lds(exp_t, log_t, aug[i * w2 + d + r],
+                                  matrix[(size_t)valid[kd + r] * k + valid[cc]]);
+            X[e] = acc;
         }
         __syncthreads();
     }
     uint8_t *tab = c.coefs + (size_t)slot * c.coef_stride;
     const int nrows = (nm + rt - 1) / rt * rt;  // pad the last pass with zero rows
     for (int e = tid; e < nrows * k; e += nt) {
-        const int t = e / k, col = e - t * k;
+        const int t = e / k, j = e - t * k;
         const int row = t < nm ? missing[t] : -1;
-        uint8_t coef;
+        uint8_t coef = 0;
         if (row < 0) {
             coef = 0;
-        } else if (row < k) {
-            coef = aug[row * w2 + k + col];
-        } else {
-            coef = 0;
+        } else if (row < k) {   // missing data row t (t < d)
+            coef = j < kd ? X[t * kd + j] : aug[t * w2 + d + (j - kd)];
+        } else {                // missing parity row: M[row] times the decode rows
             const uint8_t *mr = matrix + (size_t)row * k;
-            for (int j = 0; j < k; ++j) coef ^= gf_mul_lds(exp_t, log_t, mr[j], aug[j * w2 + k + col]);
+            if (j < kd) {
+                coef = mr[valid[j]];
+                for (int i = 0; i < d; ++i) coef ^= gf_mul_lds(exp_t, log_t, mr[missing[i]], X[i * kd + j]);
+            } else {
+                for (int i = 0; i < d; ++i)
+                    coef ^= gf_mul_lds(exp_t, log_t, mr[missing[i]], aug[i * w2 + d + (j - kd)]);
+            }
         }
-        tab[((size_t)(t / rt) * k + col) * 16 + (t % rt)] = coef;  // [pass][j][16]
+        tab[((size_t)(t / rt) * k + j) * 16 + (t % rt)] = coef;  // [pass][j][16]
     }
     for (int j = tid; j < k; j += nt) c.in_idx[(size_t)slot * k + j] = valid[j];
     for (int t = tid; t < nm; t += nt) c.out_idx[(size_t)slot * m + t] = missing[t];
@@ -1346,18 +1376,18 @@ hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     for (int i = 0; i < 8; ++i) spec.mask[i] = a.spec_mask[i];
     hipLaunchKernelGGL(pattern_lookup_kernel, dim3(grid_for(a.count, (size_t)1 << 30)),
                        dim3(kBlock), 0, s, a.n, a.present, a.count, a.cache, a.pat, a.own, spec);
-    const size_t lds = 1600 + (size_t)a.k * 2 * a.k;
-    // threads per instance by system size (measured per step): k = 22 one
-    // wave, 0.46 -> 0.34 ms (no cross-wave barriers, more instances per CU);
-    // k = 44 four waves (one: 1.42, two: 1.08, four: 1.04, eight: 1.22 ms);
-    // k = 84 eight waves (four: 1.60, eight: 1.19, sixteen: 1.23 ms).
+    const size_t lds = 1600 + (size_t)a.k * 3 * a.k;
+    // threads per instance by system size (measured per step, round 2, full
+    // k x 2k inversion): k = 22 one wave, 0.46 -> 0.34 ms; k = 84 eight waves
+    // (four: 1.60, eight: 1.19, sixteen: 1.23 ms).  Round 3 (d x d inversion,
+    // cfg4 random patterns): k = 44 two waves (one 0.48, two 0.36, four 0.39).
     // HBRBC_DM_THREADS=64..1024 forces a size.
     static const int force = [] {
         const char *e = getenv("HBRBC_DM_THREADS");
         return e ? atoi(e) : 0;
     }();
     const int threads = (force >= 64 && force <= 1024 && force % 64 == 0) ? force
-                                                                         : (a.k <= 32 ? 64 : a.k <= 64 ? 256 : 512);
+                                                                         : (a.k <= 32 ? 64 : a.k <= 64 ? 128 : 512);
     hipLaunchKernelGGL(decode_matrix_kernel, dim3((unsigned)a.count), dim3(threads), lds, s, a.n,
                        a.k, a.rt, a.matrix, a.present, a.cache, a.pat, a.own);
     hipLaunchKernelGGL(pattern_status_kernel, dim3(grid_for(a.count, (size_t)1 << 30)),
