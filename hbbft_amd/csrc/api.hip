@@ -646,7 +646,7 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v20.co";   // v20: _uf variants store the payload at any byte alignment
+           "_v23.co";   // v21: _uf variants store the payload at any byte alignment (dwords where aligned)
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
@@ -1105,8 +1105,9 @@ int decode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &r
                                roots, root_stride, shards, shard_len, rows, inst_stride, c->k,
                                count, payload_len_out, status_out, s));
     if (fused)
-        HB_HIP(launch_unframe_fixup((uint32_t)shard_len, (uint32_t)c->k, count, payload_len_out,
-                                    status_out, payload_out, payload_stride, s));
+        HB_HIP(launch_unframe_fixup(shards, (uint32_t)shard_len, rows, inst_stride, (uint32_t)c->k,
+                                    count, payload_len_out, status_out, payload_out,
+                                    payload_stride, s));
     else
         HB_HIP(launch_unframe(shards, shard_len, rows, inst_stride, c->k, count, payload_len_out,
                               status_out, payload_out, payload_stride, s));

@@ -27,7 +27,7 @@
 // (tests compare both with the oracle).
 //
 // Code objects are cached as files under <lib dir>/jit (names from
-// encode_kernel_name / decode_kernel_name + "_v20.co");
+// encode_kernel_name / decode_kernel_name + "_v23.co");
 // __graft_entry__.build() pre-generates the encoders of the BASELINE
 // validator counts and the decoders the bench's fixed patterns need.
 #include <hip/hip_runtime.h>
@@ -97,26 +97,20 @@ __device__ __forceinline__ void hb_frame_head2(const u32x4 qa, unsigned P, unsig
     _Pragma("unroll") for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], lb);
 }
 // Fused unframe (the `_uf` decoder variants only): 16 bytes of data row `row`
-// at byte `pos` are payload bytes row*S + pos - 4 .. +15: one 16-byte store at
-// any byte alignment inside the row (global memory in unaligned mode), the
-// 4-byte length prefix and the row's last chunk byte by byte (the bytes past
-// S belong to the next row's writer; the row padding is not payload) --
-// kernels.hip unframe_put.  Any payload code in a decoder slows it even when
-// unused (a branch splits the straight-line program; dropped buffer stores
-// still hold the load pipeline's vmcnt waits), so the plain decoders carry
-// none and a call that fuses loads the _uf programs.
+// at byte `pos` are payload bytes row*S + pos - 4 .. +15.  Whole chunks inside
+// the payload go as one 16-byte store at any byte alignment (global memory in
+// unaligned mode); the edge chunks (length prefix, each row's partial last
+// chunk) are copied from the shard rows by the fixup kernel -- kernels.hip
+// unframe_put.  Any payload code in a decoder slows it even when unused (a
+// branch splits the straight-line program; dropped buffer stores still hold
+// the load pipeline's vmcnt waits), so the plain decoders carry none and a
+// call that fuses loads the _uf programs.
 typedef unsigned int hb_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ void hb_uf_put(uint8_t *pb, unsigned S, unsigned row, unsigned pos,
                                           uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    if (pos >= S) return;
     const long dst = (long)row * S + pos - 4;
-    if (dst >= 0 && pos + 16u <= S) {
+    if (pos + 16u <= S && dst >= 0)
         *reinterpret_cast<hb_u32x4_a1 *>(pb + dst) = (hb_u32x4_a1){a, b, c, d};
-        return;
-    }
-    const uint32_t w[4] = {a, b, c, d};
-    _Pragma("unroll") for (int q = 0; q < 16; ++q)
-        if (pos + q < S && dst + q >= 0) pb[dst + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
 }
 // 8x32 bit transpose of 8 dwords (three delta swaps; an involution)
 __device__ __forceinline__ void hb_tr(uint32_t (&w)[8]) {

@@ -213,26 +213,20 @@ __device__ __forceinline__ void bs_transpose(uint32_t (&w)[8]) {
 }
 
 // Fused unframe (decode_from_shards, broadcast.rs:590-598): 16 bytes of data
-// row `row` at byte `pos` are payload bytes row*S + pos - 4 .. +15.  Inside
-// the row one 16-byte store at any byte alignment (the AMDGPU ABI runs global
-// memory in unaligned mode, and hipcc emits global_store_dwordx4 for it); the
-// 4-byte length prefix (row 0) and the row's last chunk, whose bytes past S
-// belong to the next row's writer, go byte by byte.  Bytes of the row padding
-// (pos >= S) are not payload.  The fixup after the root check zero-fills past
-// the length.
+// row `row` at byte `pos` are payload bytes row*S + pos - 4 .. +15.  Only the
+// chunks wholly inside the payload are written here, as one 16-byte store at
+// any byte alignment (the AMDGPU ABI runs global memory in unaligned mode, and
+// hipcc emits global_store_dwordx4 for it).  The edge chunks -- row 0's first
+// (the 4-byte length prefix) and each row's partial last chunk, whose bytes
+// past S belong to the next row's writer -- are left to unframe_fixup_kernel,
+// which copies them from the rebuilt shard rows: byte stores at every call
+// site grew this kernel 2.5x and cost 7-20% of the reconstruct at cfg3.
 typedef uint32_t hb_u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ void unframe_put(uint8_t *pb, uint32_t S, uint32_t row, uint32_t pos,
                                             uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    if (pos >= S) return;
     const int64_t dst = (int64_t)row * S + pos - 4;
-    if (dst >= 0 && pos + 16 <= S) {
+    if (pos + 16 <= S && dst >= 0)
         *reinterpret_cast<hb_u32x4_a1 *>(pb + dst) = (hb_u32x4_a1){a, b, c, d};
-        return;
-    }
-    const uint32_t w[4] = {a, b, c, d};
-#pragma unroll
-    for (int q = 0; q < 16; ++q)
-        if (pos + q < S && dst + q >= 0) pb[dst + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
 }
 
 template <int RT, int MODE>
@@ -1409,17 +1403,31 @@ hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes
     return hipGetLastError();
 }
 
-// Fixup after a fused-unframe reconstruct (gf_bitslice_kernel wrote payload
-// bytes [0, k*S - 4) of every instance whose reconstruct succeeded): zero the
-// bytes past the decoded length, or the whole slot of a failed instance, so
-// the payload buffer ends exactly as unframe_kernel leaves it.  One workgroup
-// per instance; honest instances touch one or two chunks.
+// Fixup after a fused-unframe reconstruct (gf_bitslice_kernel wrote the
+// whole 16-byte chunks of payload bytes [0, k*S - 4) of every instance whose
+// reconstruct succeeded).  Phase 1 copies the edge bytes below the decoded
+// length from the shard rows: row 0's bytes 4..15 and every row's bytes past
+// its last whole chunk (S & ~15 .. S-1).  Phase 2 zeroes the bytes past the
+// length, or the whole slot of a failed instance, so the payload buffer ends
+// exactly as unframe_kernel leaves it.  One workgroup per instance.
 __global__ __launch_bounds__(kBlock) void unframe_fixup_kernel(
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride, uint32_t k,
     uint32_t chunks, const uint32_t *__restrict__ plen, const int32_t *__restrict__ status,
     uint8_t *__restrict__ payload_out, size_t payload_stride) {
     const size_t inst = blockIdx.x;
     const uint32_t len = status[inst] == 0 ? plen[inst] : 0u;
     uint8_t *pb = payload_out + inst * payload_stride;
+    if (len) {
+        const uint8_t *ib = shards + inst * inst_stride;
+        const uint32_t tail0 = S & ~15u;
+        for (uint32_t i = threadIdx.x; i < 16 * (k + 1); i += kBlock) {
+            const uint32_t r = i < 16 ? 0u : (i - 16) >> 4;
+            const uint32_t pos = i < 16 ? i : tail0 + (i & 15);
+            const uint32_t p = r * S + pos - 4;   // payload index (k*S < 2^32)
+            if (pos < S && r * S + pos >= 4 && p < len) pb[p] = ib[rows.off(r) + pos];
+        }
+        __syncthreads();
+    }
     for (uint32_t c = len / 16 + threadIdx.x; c < chunks; c += kBlock) {
         const uint32_t o = c * 16;
         uint4 *dst = reinterpret_cast<uint4 *>(pb + o);
@@ -1440,15 +1448,16 @@ __global__ __launch_bounds__(kBlock) void unframe_fixup_kernel(
     }
 }
 
-hipError_t launch_unframe_fixup(uint32_t S, uint32_t k, size_t count, const uint32_t *plen,
+hipError_t launch_unframe_fixup(const uint8_t *shards, uint32_t S, const RowMap &rows,
+                                size_t inst_stride, uint32_t k, size_t count, const uint32_t *plen,
                                 const int32_t *status, uint8_t *payload_out, size_t payload_stride,
                                 hipStream_t s) {
     const uint64_t total = (uint64_t)k * S;
     if (count == 0 || total <= 4) return hipSuccess;
-    if (count > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (count > 0x7FFFFFFFull || total + 16 >= ((uint64_t)1 << 32)) return hipErrorInvalidValue;
     const uint32_t chunks = (uint32_t)((total - 4 + 15) / 16);
-    hipLaunchKernelGGL(unframe_fixup_kernel, dim3((unsigned)count), dim3(kBlock), 0, s, chunks,
-                       plen, status, payload_out, payload_stride);
+    hipLaunchKernelGGL(unframe_fixup_kernel, dim3((unsigned)count), dim3(kBlock), 0, s, shards, S,
+                       rows, inst_stride, k, chunks, plen, status, payload_out, payload_stride);
     return hipGetLastError();
 }
 

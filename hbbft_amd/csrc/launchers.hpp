@@ -190,7 +190,8 @@ hipError_t launch_decode_check(const int32_t *recon_status, const uint8_t *nodes
                                hipStream_t s);
 // After a fused-unframe reconstruct: zero payload bytes past the decoded
 // length (all of them for a failed instance), as unframe_kernel leaves them.
-hipError_t launch_unframe_fixup(uint32_t S, uint32_t k, size_t count, const uint32_t *plen,
+hipError_t launch_unframe_fixup(const uint8_t *shards, uint32_t S, const RowMap &rows,
+                                size_t inst_stride, uint32_t k, size_t count, const uint32_t *plen,
                                 const int32_t *status, uint8_t *payload_out, size_t payload_stride,
                                 hipStream_t s);
 hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, const RowMap &rows,
