@@ -1218,7 +1218,9 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     switch (a.rt) {
         HB_BS_CASE(2);
         HB_BS_CASE(4);
+        HB_BS_CASE(5);
         HB_BS_CASE(6);
+        HB_BS_CASE(7);
         HB_BS_CASE(8);
         HB_BS_CASE(10);
         HB_BS_CASE(12);

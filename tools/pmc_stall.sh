@@ -11,9 +11,12 @@ mkdir -p $OUT
 REGEX=${REGEX:-hbrbc_enc|hbrbc_dec|gf_bitslice|leaf_hash|validate_kernel}
 ARGS="--config ${CONFIG:-cfg3} --steps 1 --warmup 1 --no-cpu --mode instances --no-verify"
 i=0
-for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" \
+# SETS="group1|group2|..." replaces the default counter groups
+if [ -n "$SETS" ]; then IFS='|' read -r -a GROUPS_ <<< "$SETS"; else GROUPS_=(); fi
+if [ ${#GROUPS_[@]} -gt 0 ]; then set -- "${GROUPS_[@]}"; else set -- "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" \
          "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD" \
-         "FETCH_SIZE" "WRITE_SIZE"; do
+         "FETCH_SIZE" "WRITE_SIZE"; fi
+for C in "$@"; do
   i=$((i+1))
   timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex "$REGEX" --output-format csv -d $OUT/p$i -o run -- python3 $ROOT/bench.py $ARGS > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i exit $rc"
