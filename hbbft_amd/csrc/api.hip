@@ -772,7 +772,12 @@ int spec_row_tile(size_t nin, size_t nout) {
     // a one-program matrix with more than 56 outputs takes longer passes so
     // that one workgroup holds them all (<= 8 waves; cfg4: 84 rows, 11 per pass)
     if (spec_lds(nin, nout)) {
-        if (nin * nout > 4096) return 7;   // split programs: groups of <= 48 rows
+        // split programs: 48-row groups in eight 6-row passes, one wave each
+        // (cfg5 r3, same box: encode 10.0 -> 9.1 ms, worst-case reconstruct
+        // 9.7 -> 8.8 ms against 42-row groups in six 7-row passes; 8-row
+        // passes 9.9 / 9.5 ms; LDS stages of 12 / 16 / 28 inputs flat / flat /
+        // 12.1 / 12.0 ms)
+        if (nin * nout > 4096) return 6;
         return (int)std::max<size_t>(7, (nout + 7) / 8);
     }
     // split matrices (N = 250): 12-row passes of the pairwise network, four

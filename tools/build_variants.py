@@ -6,7 +6,8 @@ code object so no knob leaks from one build into the next.
 usage: python tools/build_variants.py 'ENV=V[,ENV=V...]' [...] --n 64 [--dec] [-j 8]
   each positional argument is one variant, e.g. HBRBC_RT_SPEC=8 or
   HBRBC_RT_SPEC=14,HBRBC_JIT_FDEPTH=4; --n picks the validator count (f =
-  (n-1)//3); --dec also builds the decoders of the bench's fixed patterns for n.
+  (n-1)//3); --dec also builds the decoders of the bench's fixed patterns for n,
+  --uf their fused-unframe variants.
 """
 import argparse
 import os
@@ -24,7 +25,7 @@ kind, k, m, g, pres = json.loads(sys.argv[1])
 if kind == "enc":
     hb.jit_build_encode(k, m, group=g)
 else:
-    hb.jit_build_decode(k, m, pres, g)
+    hb.jit_build_decode(k, m, pres, g, fused_unframe=kind == "decuf")
 """
 
 
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("variants", nargs="+")
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--dec", action="store_true")
+    ap.add_argument("--uf", action="store_true", help="also the fused-unframe (_uf) decoders")
     ap.add_argument("-j", type=int, default=8)
     a = ap.parse_args()
     sys.path.insert(0, ROOT)
@@ -53,6 +55,8 @@ def main():
         jobs += [(env, v, ["enc", k, m, g, None]) for g in range(ne)]
         if a.dec:
             jobs += [(env, v, ["dec", k, m, g, pres]) for g in range(nd)]
+        if a.uf:
+            jobs += [(env, v, ["decuf", k, m, g, pres]) for g in range(nd)]
 
     def run(job):
         env, v, t = job
