@@ -777,7 +777,10 @@ int spec_row_tile(size_t nin, size_t nout) {
         // 9.7 -> 8.8 ms against 42-row groups in six 7-row passes; 8-row
         // passes 9.9 / 9.5 ms; LDS stages of 12 / 16 / 28 inputs flat / flat /
         // 12.1 / 12.0 ms)
-        if (nin * nout > 4096) return 6;
+        // Same for a one-program matrix of more than 56 rows (xor_groups caps
+        // a program at eight passes): cfg4 encode, 84 rows in 48 + 36 instead
+        // of one program of 11-row passes at 3 waves/SIMD, 2.9 -> 2.57 ms
+        if (nin * nout > 4096 || nout > 56) return 6;
         return (int)std::max<size_t>(7, (nout + 7) / 8);
     }
     // split matrices (N = 250): 12-row passes of the pairwise network, four
@@ -1166,6 +1169,8 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
         // 7-row passes where they save a pass (N=64: 21 rows in 7, 7, 7 instead
         // of 6, 6, 6, 3; reconstruct 3.61 -> 3.44 ms per step, round 3)
         if (c->rt_rec == 6 && (h + 6) / 7 < (h + 5) / 6) c->rt_rec = 7;
+        // and 7-row passes up to N=128 (h = 42: 12 -> 7, 3.45 -> 3.06 ms; 10: 3.17)
+        if (h >= 14 && h <= 42) c->rt_rec = 7;
     }
     if (const char *e = getenv("HBRBC_GF")) {
         // bitslice (uniform branches), bitslice_likely (set-bit path inline),

@@ -679,6 +679,10 @@ std::vector<std::pair<int, int>> xor_groups(size_t nin, size_t nout, int rt) {
     std::vector<std::pair<int, int>> g;
     size_t per = nout;
     if (nin * nout > kMaxCoefs) per = std::max<size_t>((size_t)rt, kMaxCoefs / nin / rt * rt);
+    // short passes of the LDS form (api.hip spec_lds: >= 16 inputs): at most
+    // eight per program (one wave each, the form's limit), so 84 rows of 6-row
+    // passes are two programs, 48 + 36
+    if (nin >= 16 && rt <= 8) per = std::min(per, (size_t)(8 * rt));
     for (size_t lo = 0; lo < nout; lo += per) g.push_back({(int)lo, (int)std::min(nout, lo + per)});
     return g;
 }
