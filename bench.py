@@ -72,6 +72,8 @@ def parse():
                     help="skip the cfg4 validator-sharded object of the default cfg3 line")
     ap.add_argument("--streams", type=int, default=1,
                     help="instance mode: sub-batches per step, each on its own HIP stream")
+    ap.add_argument("--stagger", action="store_true",
+                    help="with --streams > 1: each sub-batch starts after the previous one's encode")
     ap.add_argument("--vsubs", type=int, default=4,
                     help="validator mode with >1 rank: pipelined sub-batches per step")
     ap.add_argument("--mode", choices=["instances", "validators", "both"], default="both",
@@ -359,8 +361,10 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
         sb.reserve(hi - lo)
         subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
 
-    def run_sub(sb, sl, pres):
+    def run_sub(sb, sl, pres, after_encode=None):
         sb.frame_encode(payloads[sl], plen, slab[sl])   # frame folded into the encoder
+        if after_encode is not None:
+            after_encode()
         sb.merkle(slab[sl], S, nodes[sl])
         sb.proofs(nodes[sl], digests[sl], ndig[sl])
         sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
@@ -375,10 +379,18 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
             return
         ev = torch.cuda.Event()
         ev.record(main)
+        prev = ev
         for sb, st, sl in subs:
-            st.wait_event(ev)
+            st.wait_event(prev)
             with torch.cuda.stream(st):
-                run_sub(sb, sl, pres)
+                if args.stagger:
+                    # the next sub-batch starts when this one's encode is done:
+                    # its encode (HBM-heavy) runs beside this one's sponges
+                    nxt = torch.cuda.Event()
+                    run_sub(sb, sl, pres, after_encode=lambda: nxt.record(st))
+                    prev = nxt
+                else:
+                    run_sub(sb, sl, pres)
         for _, st, _ in subs:
             main.wait_stream(st)
 

@@ -9,8 +9,9 @@ HBRBC_JIT=load TAG=r3f BENCH_ARGS="--steps 5 --warmup 1 --no-cpu --mode instance
 rc=$?; echo "profile exit $rc"; if fatal $rc; then exit $rc; fi
 # two sub-batches on two streams (re-measured now that encode / reconstruct are
 # closer to HBM-bound than VALU-bound)
-for ns in 2 1; do
-  HBRBC_JIT=load timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu --mode instances --f4-checks 0 --streams $ns > gpurun_out/r3f_streams$ns.log 2>&1
+for ns in "2" "2 --stagger" "4 --stagger" "1"; do
+  tag=$(echo "$ns" | tr -d ' -')
+  HBRBC_JIT=load timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu --mode instances --f4-checks 0 --streams $ns > gpurun_out/r3f_streams$tag.log 2>&1
   rc=$?; echo "streams $ns exit $rc"; if fatal $rc; then exit $rc; fi
 done
 SKIP_TESTS=1 TAG=r3f bash tools/gpu_round.sh
