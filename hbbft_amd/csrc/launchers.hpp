@@ -251,12 +251,14 @@ hipError_t launch_pairing_final(const uint32_t *ws, size_t n_miller, size_t n_ou
 hipError_t configure_kernels();
 
 // Broadcast state machine rounds (sim.hip).  Bytes per node: er u16[n]
-// (echo | ready << 8), can_decodes u32[roots][W], full Echoes u32[W], counters u16[3][roots],
-// flags u32, + 6 of alignment slack for a block, rounded to 8; an instance's
-// block holds its hosted nodes' fields as structures of arrays.
+// (echo | ready << 8; u8[n], echo | ready << 6, with one root), can_decodes
+// u32[roots][W], full Echoes u32[W], counters u16[3][roots], flags u32, + 6 of
+// alignment slack for a block, rounded to 8; an instance's block holds its
+// hosted nodes' fields as structures of arrays.
+__host__ __device__ inline size_t sm_er_bytes(size_t n, size_t roots) { return roots == 1 ? n : 2 * n; }
 __host__ __device__ inline size_t sm_state_bytes(size_t n, size_t roots) {
     const size_t w = (n + 31) / 32;
-    return (2 * n + 4 * roots * w + 4 * w + 6 * roots + 4 + 6 + 7) & ~(size_t)7;
+    return (sm_er_bytes(n, roots) + 4 * roots * w + 4 * w + 6 * roots + 4 + 6 + 7) & ~(size_t)7;
 }
 hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s);
 

@@ -73,7 +73,8 @@ enum : uint32_t {
 // Per sender s a node keeps one 16-bit word (er[s]): bits 0..7 the echo
 // entry (EchoContent) -- 0 none, Hash: 0x10 | c, Full: 0x20 | t << 3 | c (a
 // stored full Echo is always proof index s, validate_proof checks it) -- and
-// bits 8..11 the Ready entry (root + 1, 0 none).
+// bits 8..11 the Ready entry (root + 1, 0 none).  With one root (c = 0) the
+// entry fits a byte: echo in bits 0..5, Ready in bits 6..7 (Sm<true>).
 __device__ __forceinline__ uint32_t enc_full(uint32_t c, uint32_t t) {
     return 0x20u | ((t & 1u) << 3) | (c & 7u);
 }
@@ -97,7 +98,11 @@ struct Sm {
     // state of (inst, me), structure of arrays over the instance's hosted
     // nodes (stride sd = nodes): the nodes of an instance are consecutive
     // threads, so every state access of a wave is one coalesced request
-    uint16_t *er;             // [n][sd]: echo entry | ready entry << 8
+    // [n][sd]: echo entry | ready entry << 8 (er16), or with one root (ONE:
+    // every root index is 0, so ready = 1) echo entry | ready << 6 in a byte
+    // (er8): half the LDS image, more resident workgroups
+    uint16_t *er16;
+    uint8_t *er8;
     uint32_t *cand;           // [C][W][sd]
     uint32_t *full;           // [W][sd]: senders whose entry is a full Echo
     uint16_t *cnt;            // [3][C][sd]: Echo+EchoHash, full Echo, Ready counts
@@ -106,15 +111,31 @@ struct Sm {
     const uint8_t *pok;       // this instance's proof_ok [C][2][n]
     const uint8_t *dok;       // this instance's decode_ok [C]
 
-    __device__ uint32_t ECHO(int s) const { return er[(size_t)s * sd] & 0xFFu; }
-    __device__ void set_echo(int s, uint32_t e) {
-        uint16_t &w = er[(size_t)s * sd];
-        w = (uint16_t)((w & 0xFF00u) | e);
+    __device__ uint32_t ECHO(int s) const {
+        if constexpr (ONE) return er8[(size_t)s * sd] & 0x3Fu;
+        else return er16[(size_t)s * sd] & 0xFFu;
     }
-    __device__ uint32_t READY(int s) const { return er[(size_t)s * sd] >> 8; }
+    __device__ void set_echo(int s, uint32_t e) {
+        if constexpr (ONE) {
+            uint8_t &b = er8[(size_t)s * sd];
+            b = (uint8_t)((b & 0xC0u) | e);
+        } else {
+            uint16_t &w = er16[(size_t)s * sd];
+            w = (uint16_t)((w & 0xFF00u) | e);
+        }
+    }
+    __device__ uint32_t READY(int s) const {
+        if constexpr (ONE) return er8[(size_t)s * sd] >> 6;
+        else return er16[(size_t)s * sd] >> 8;
+    }
     __device__ void set_ready(int s, uint32_t r) {
-        uint16_t &w = er[(size_t)s * sd];
-        w = (uint16_t)((w & 0xFFu) | (r << 8));
+        if constexpr (ONE) {
+            uint8_t &b = er8[(size_t)s * sd];
+            b = (uint8_t)((b & 0x3Fu) | (r << 6));
+        } else {
+            uint16_t &w = er16[(size_t)s * sd];
+            w = (uint16_t)((w & 0xFFu) | (r << 8));
+        }
     }
     __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
     __device__ uint32_t &FULL(int w) { return full[(size_t)w * sd]; }
@@ -428,12 +449,13 @@ __device__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {  
 
 // Byte offsets of the fields of an instance's state block holding `sd` nodes
 // as structures of arrays (include/hbrbc.h hbrbc_sm_state_bytes, per node:
-// er u16[n], cand u32[C][W], full u32[W], counters u16[3][C], flags u32).
+// er u16[n] (u8[n] with one root), cand u32[C][W], full u32[W], counters
+// u16[3][C], flags u32).
 struct SmLayout {
     size_t er, cand, full, cnt, flags;
     __device__ SmLayout(int n, int C, int W, size_t sd) {
         er = 0;
-        cand = (2 * (size_t)n * sd + 3) & ~(size_t)3;
+        cand = (sm_er_bytes((size_t)n, (size_t)C) * sd + 3) & ~(size_t)3;
         full = cand + 4 * (size_t)C * W * sd;
         cnt = full + 4 * (size_t)W * sd;
         flags = (cnt + 6 * (size_t)C * sd + 3) & ~(size_t)3;
@@ -463,7 +485,8 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
     m.proposer = a.proposer[inst];
     m.role = a.role[inst * n + me];
     m.sd = sd;
-    m.er = reinterpret_cast<uint16_t *>(st + L.er) + local;
+    m.er16 = reinterpret_cast<uint16_t *>(st + L.er) + local;
+    m.er8 = st + L.er + local;
     m.cand = reinterpret_cast<uint32_t *>(st + L.cand) + local;
     m.full = reinterpret_cast<uint32_t *>(st + L.full) + local;
     m.cnt = reinterpret_cast<uint16_t *>(st + L.cnt) + local;
