@@ -82,3 +82,20 @@ def test_no_cpu_fallback_without_gpu():
     assert hb.lib().hbrbc_coding_new(4, 2, -1, ctypes.byref(ctypes.c_void_p())) == 102
     with pytest.raises(hb.HbrbcUnavailable):
         hb.RbcBatch(16)
+
+
+def test_state_machine_block_size():
+    """hbrbc_sm_state_bytes (include/hbrbc.h): per node, the echo/ready entry
+    of every sender (one byte with one root, two otherwise), can_decode and
+    full-Echo masks, counters and flags, rounded to 8 bytes."""
+    import hbbft_amd.rbc_sim  # noqa: F401  (declares the restype)
+    L = hb.lib()
+    L.hbrbc_sm_state_bytes.restype = ctypes.c_size_t
+    L.hbrbc_sm_state_bytes.argtypes = [ctypes.c_size_t, ctypes.c_size_t]
+    for n in (1, 4, 16, 31, 64, 128, 250):
+        w = (n + 31) // 32
+        for roots in (1, 2, 3):
+            er = n if roots == 1 else 2 * n
+            want = (er + 4 * roots * w + 4 * w + 6 * roots + 4 + 6 + 7) & ~7
+            got = L.hbrbc_sm_state_bytes(n, roots)
+            assert got == want and got % 8 == 0, (n, roots, got, want)
