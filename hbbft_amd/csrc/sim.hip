@@ -573,8 +573,8 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
 // count, flags, outcome, ...) then cost LDS latency instead of an L2 round
 // trip each.  The state goes back at the end.
 template <bool ONE>
-__global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
-                                                             int k, int ipb) {
+__device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, int f, int k,
+                                                int ipb) {
     extern __shared__ uint4 sm_lds4[];
     uint8_t *lds = reinterpret_cast<uint8_t *>(sm_lds4);
     const int T = (int)blockDim.x, tid = (int)threadIdx.x;
@@ -627,6 +627,21 @@ __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, i
         reinterpret_cast<uint2 *>(gst)[i] = reinterpret_cast<const uint2 *>(lds)[i];
 }
 
+template <bool ONE>
+__global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
+                                                              int k, int ipb) {
+    sm_round_staged<ONE>(a, n, f, k, ipb);
+}
+// The same at 4 waves/SIMD (128 VGPRs, a few spills instead of 162 VGPRs):
+// for launches whose LDS image leaves room for more than 3 waves per SIMD
+// (N=64 validator-sharded object: state machine 0.82 -> 0.63 ms per step;
+// at N=128 the LDS holds 2 waves per SIMD and the spills cost 1.25 -> 1.28)
+template <bool ONE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void
+sm_round_staged_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
+    sm_round_staged<ONE>(a, n, f, k, ipb);
+}
+
 }  // namespace
 
 // Launch plan: the staged form with ipb instances per workgroup (ipb x nodes
@@ -648,14 +663,15 @@ hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStrea
     while (ipb > 1 && sm_lds_bytes(a, n, ipb) > 65536) --ipb;
     if (staged_ok && sm_lds_bytes(a, n, ipb) <= 65536) {
         const unsigned blocks = (unsigned)((a.count + ipb - 1) / ipb);
-        if (a.roots == 1)
-            hipLaunchKernelGGL(sm_round_staged_kernel<true>, dim3(blocks),
-                               dim3((unsigned)(ipb * a.nodes)), sm_lds_bytes(a, n, ipb), s, a, n,
-                               f, k, ipb);
-        else
-            hipLaunchKernelGGL(sm_round_staged_kernel<false>, dim3(blocks),
-                               dim3((unsigned)(ipb * a.nodes)), sm_lds_bytes(a, n, ipb), s, a, n,
-                               f, k, ipb);
+        const size_t lds = sm_lds_bytes(a, n, ipb), threads_pb = (size_t)ipb * a.nodes;
+        // waves per CU the LDS image allows (160 KiB per CU) above 3 per SIMD:
+        // the 4-wave form (HBRBC_SM_W4=0/1 forces, A/B)
+        const char *w4e = getenv("HBRBC_SM_W4");
+        const bool w4 = w4e ? !strcmp(w4e, "1")
+                            : (163840 / lds) * ((threads_pb + 63) / 64) > 12;
+        auto kern = a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true> : sm_round_staged_kernel<true>)
+                                 : (w4 ? sm_round_staged_w4_kernel<false> : sm_round_staged_kernel<false>);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3((unsigned)threads_pb), lds, s, a, n, f, k, ipb);
         return hipGetLastError();
     }
     const unsigned blocks = (unsigned)((threads + 255) / 256);
