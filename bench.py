@@ -74,6 +74,8 @@ def parse():
                     help="instance mode: sub-batches per step, each on its own HIP stream")
     ap.add_argument("--stagger", action="store_true",
                     help="with --streams > 1: each sub-batch starts after the previous one's encode")
+    ap.add_argument("--no-leaf-reuse", action="store_true",
+                    help="skip the instance-mode leaf_reuse variant (labelled, not the headline)")
     ap.add_argument("--vsubs", type=int, default=4,
                     help="validator mode with >1 rank: pipelined sub-batches per step")
     ap.add_argument("--mode", choices=["instances", "validators", "both"], default="both",
@@ -232,7 +234,7 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
          "pipeline_hbm_frac": step_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS,
          "pipeline_frac_of_measured_copy": step_bytes / (elapsed / steps) / 1e9 / HBM_COPY_GBS}
     if dom in perms:
-        opp, src = valu_ops_per_perm()
+        opp, src = valu_ops_per_perm(config)
         pps = perms[dom] / t
         ops = pps * opp / 1e12
         r.update({"bound": "valu", "achieved": ops, "peak": VALU_PEAK_OPS / 1e12,
@@ -247,14 +249,15 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
     return r
 
 
-def valu_ops_per_perm():
+def valu_ops_per_perm(config):
     """32-bit lane-ops per Keccak-f[1600] of the sponge kernel: SQ_INSTS_VALU x 64
-    / permutations from the committed counter pass, else the static count."""
+    / permutations from the committed counter pass of THIS config
+    (profiles/valu_ops_per_perm.json, keyed by config), else the static count."""
     p = os.path.join(ROOT, "profiles", "valu_ops_per_perm.json")
     try:
-        d = json.load(open(p))
+        d = json.load(open(p))[config]
         return float(d["leaf_hash_kernel"]), "rocprofv3 SQ_INSTS_VALU (%s)" % d["source"]
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError, KeyError, TypeError):
         return float(KECCAK_OPS_PER_PERM), "static: 180 VALU/round x 24"
 
 
@@ -440,6 +443,10 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
     value = float(count) * plen * world * args.steps / elapsed / 1e9
+    lr = None
+    if not args.no_leaf_reuse and nsub == 1 and erase == "f":
+        lr = run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests,
+                            ndig, ok, out, plen_out, status, S, n, f, world, dev)
     roof = roofline_of(stages, args.steps, count / nsub, n, k, m, S, plen, rb.node_count,
                        rb.dslots, n_erase, elapsed, args.config,
                        unframe_fused=rb.unframe_fused(S, out.stride(0)))
@@ -453,8 +460,79 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
                    "n": n, "f": f, "payload_bytes": plen, "shard_len": S,
                    "instances_per_gpu": count, "global_batch": count * world,
                    "parallelism": "instance-sharded x%d" % world, "streams_per_gpu": nsub},
-        "n_erase": n_erase, "f": f,
+        "n_erase": n_erase, "f": f, "leaf_reuse": lr,
     }
+
+
+def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests, ndig,
+                   ok, out, plen_out, status, S, n, f, world, dev):
+    """Labelled variant of the instance step, NOT the headline: validate
+    writes each validated row's Merkle leaf into the decode tree
+    (hbrbc_validate_rows leaf_out), and the decode hashes only the rows the
+    reconstruct rebuilds (known_leaves).  A node can do exactly this with
+    the Echoes it validated (broadcast.rs:291 validate_proof, then 580
+    MerkleTree::from_vec over the same rows); the reference hashes them
+    again.  Same inputs, same erasure patterns, same outputs."""
+    import torch
+    count = slab.shape[0]
+
+    def step(i):
+        pres = pool[i % len(pool)]
+        rb.frame_encode(payloads, plen, slab)
+        rb.merkle(slab, S, nodes)
+        rb.proofs(nodes, digests, ndig)
+        rb.validate(slab, S, digests, ndig, nodes, ok, leaf_out=nodes2)
+        roots.copy_(nodes[:, -1, :])
+        rb.decode(slab, S, pres, roots, nodes2, out, plen_out, status, known_leaves=True)
+
+    for i in range(max(1, args.warmup)):
+        step(i)
+    torch.cuda.synchronize(dev)
+    verified = False
+    if not args.no_verify:
+        assert bool((ok == 1).all()) and bool((status == 0).all())
+        assert torch.equal(out[:, :plen], payloads[:, :plen]), "leaf reuse: payload differs"
+        # garbage in the erased rows AND in their leaves: the decode must
+        # rebuild both (the present rows' leaves come from validate)
+        present = pool[(max(1, args.warmup) - 1) % len(pool)]
+        rb.validate(slab, S, digests, ndig, nodes, ok, leaf_out=nodes2)
+        vs = slab.clone()
+        vs[present == 0] = 0xA5
+        nodes2[:, :n][present == 0] = 0x5A
+        out.zero_()
+        rb.decode(vs, S, present, roots, nodes2, out, plen_out, status, known_leaves=True)
+        torch.cuda.synchronize(dev)
+        assert bool((status == 0).all()), "leaf reuse: decode from garbage failed"
+        assert torch.equal(out[:, :plen], payloads[:, :plen]), "leaf reuse: rebuilt payload differs"
+        assert torch.equal(vs, slab) and torch.equal(nodes2, nodes), "leaf reuse: rows/tree differ"
+        del vs
+        verified = True
+    rb.profile(True)
+    rb.profile_reset()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    rb.profile(False)
+    stages = {k_: v_[0] / args.steps for k_, v_ in rb.profile_read().items()}
+    bl = (S + 1 + 135) // 136          # Keccak blocks per leaf (SHA3-256 rate 136)
+    depth = max(1, (n - 1).bit_length())
+    tree = n * bl + (n - 1)
+    faithful = tree + n * (bl + depth) + tree
+    executed = tree + n * (bl + depth) + f * bl + (n - 1)
+    return {"value": float(count) * plen * world * args.steps / elapsed / 1e9, "unit": "GB/s",
+            "ms_per_step": elapsed / args.steps * 1e3, "stages_ms_per_step": stages,
+            "verified_garbage_fill": verified,
+            "keccak_perms_per_instance": {"faithful": faithful, "executed": executed},
+            "note": "labelled variant, not the headline: validate emits the Merkle leaf of each "
+                    "validated row and the decode re-hashes only the f rebuilt rows"}
 
 
 def max_over_ranks(x, world, dev):
@@ -848,6 +926,8 @@ def main():
                 "config": head["config"], "roofline": head["roofline"], "cpu_baseline": cpu,
                 "stages_ms_per_step": head["stages_ms_per_step"],
             }
+            if head.get("leaf_reuse") is not None:
+                line["leaf_reuse"] = head["leaf_reuse"]
             if cpu is None and world > 1:
                 line["cpu_baseline_note"] = ("measured on rank 0 of the N=1 run only (bench "
                                              "contract); see that line's cpu_baseline")

@@ -142,6 +142,12 @@ pub fn merkle_from_vec<T: AsRef<[u8]>>(values: &[T]) -> (Vec<Vec<[u8; 32]>>, [u8
 
 /// `Proof::validate` (merkle.rs:83-103) of (value, index, digests, root) in a
 /// tree over n leaves.  A device failure panics: it is not an invalid proof.
+///
+/// Per call this is slower than the CPU: 651 µs against 49 µs for
+/// tiny-keccak on one core at N=64 with 11,916-byte shards, 359 / 29 µs at
+/// N=128, 62 / 12 µs at N=4 (profiles/r3_percall_pair.jsonl).  One proof is a
+/// serial chain of permutations.  Batch proofs through
+/// `hbrbc_validate_batch` instead; use this only behind an opt-in feature.
 pub fn proof_validate(value: &[u8], index: usize, digests: &[[u8; 32]], root: &[u8; 32], n: usize) -> bool {
     let mut ok: c_int = 0;
     let st = unsafe {

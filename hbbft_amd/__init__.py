@@ -581,10 +581,19 @@ class RbcBatch:
                                         nodes.shape[0], _ptr(digests), _ptr(ndig),
                                         self._stream(stream)))
 
-    def validate(self, slab, S, digests, ndig, nodes, ok, indices=None, stream=None):
-        """Validate all n proofs of every instance against its own root."""
+    def validate(self, slab, S, digests, ndig, nodes, ok, indices=None, leaf_out=None,
+                 stream=None):
+        """Validate all n proofs of every instance against its own root.
+        leaf_out: a node slab [count, node_count, 32] whose level 0 receives
+        each validated row's Merkle leaf (hbrbc_validate_rows), for a decode
+        with known_leaves."""
         count = slab.shape[0]
         root = nodes[:, -1, :]
+        if leaf_out is not None:
+            self.validate_layout(slab, S, count, self.n, slab.stride(1), 0, 0, slab.stride(0),
+                                 digests, ndig, self.n, root, ok, indices=indices,
+                                 leaf_out=leaf_out, stream=stream)
+            return
         _check(lib().hbrbc_validate_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
                                           slab.stride(0), self.n, _ptr(indices), _ptr(digests),
                                           _ptr(ndig), _ptr(root), nodes.stride(0), self.n,
@@ -684,8 +693,15 @@ class RbcBatch:
                                               rows_per_block))
 
     def decode(self, slab, S, present, roots, nodes, payload_out, plen_out, status,
-               stream=None):
-        """roots: uint8 [count, >=32] (row stride multiple of 16)."""
+               known_leaves=False, stream=None):
+        """roots: uint8 [count, >=32] (row stride multiple of 16).  known_leaves:
+        level 0 of `nodes` already holds the leaves of the present rows (from
+        validate(leaf_out=nodes)); only the rebuilt rows are hashed again."""
+        if known_leaves:
+            self.decode_rows(slab, S, slab.shape[0], slab.stride(1), 0, 0, slab.stride(0),
+                             present, roots, nodes, payload_out, plen_out, status,
+                             known_leaves=True, stream=stream)
+            return
         _check(lib().hbrbc_decode_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
                                         slab.stride(0), _ptr(present), slab.shape[0],
                                         _ptr(roots), roots.stride(0), _ptr(nodes),

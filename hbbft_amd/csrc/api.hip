@@ -248,6 +248,9 @@ struct hbrbc_ctx {
         int r_lo, r_hi;
         hipModule_t mod;
         hipFunction_t fn, fe;        // kernel / frame+encode twin (encoder only)
+        // LDS-staged form (jit.hip gen_xor_kernel_lds): its waves share the
+        // stage's input planes, so it cannot run pass by pass
+        bool lds = false;
     };
     // encoder modules by code-object row block (256 = plain layout); an
     // empty vector records a failed load
@@ -646,7 +649,7 @@ std::string jit_dir() {
 std::string jit_file(const std::string &dir, const std::string &kernel) {
     const char *aux = getenv("HBRBC_ST_AUX");   // A/B builds get their own files
     return dir + "/" + kernel + (aux && std::strcmp(aux, "2") ? std::string("_a") + aux : std::string()) +
-           "_v23.co";   // v21: _uf variants store the payload at any byte alignment (dwords where aligned)
+           "_v23.co";   // v23: the reconstruct programs store whole 16-byte payload chunks only
 }
 
 // Input rows in flight of the specialised kernels (HBM latency at 2 waves/SIMD).
@@ -860,6 +863,8 @@ int load_program(const XorProgram &p, bool compile, hbrbc_ctx::SpecGroup &g) {
     }
     g.mod = nullptr;
     g.fn = g.fe = nullptr;
+    const int npass = (int)((p.out_rows.size() + p.rt - 1) / p.rt);
+    g.lds = p.lds && npass >= 2 && npass <= 8;   // the test of gen_xor_source
     HB_HIP(hipModuleLoadData(&g.mod, code.data()));
     if (hipModuleGetFunction(&g.fn, g.mod, p.name.c_str()) != hipSuccess ||
         (p.fused && hipModuleGetFunction(&g.fe, g.mod, (p.name + "_fe").c_str()) != hipSuccess)) {
@@ -927,7 +932,9 @@ hipError_t launch_xor_group(const hbrbc_ctx::SpecGroup &g, bool fused, int rt, X
                     &a.hash_slots, &a.p_only,     &a.uf_payload,   &a.uf_stride,
                     &a.uf_status};
     hipFunction_t fn = fused ? g.fe : g.fn;
-    if (!spec_pass_split()) {
+    // HBRBC_SPEC_SPLIT applies to the streaming form only: a wave of the LDS
+    // form loads just its share of each stage's inputs
+    if (!spec_pass_split() || g.lds) {
         a.p_only = -1;
         const unsigned threads = 64u * (unsigned)xor_waves(npass);
         return hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, threads, 1, 1, 0, s, args, nullptr);
@@ -1336,10 +1343,13 @@ int hbrbc_frame_encode_rows(hbrbc_ctx *c, const uint8_t *payloads, size_t payloa
     const RowMap rows = make_rows(c->n, shard_stride, rows_per_block, block_stride);
     const std::vector<hbrbc_ctx::SpecGroup> *gs = nullptr;
     if (c->m > 0 && shard_stride == round_up(shard_len, 16) && payload_len <= 0x7FFFFFFFull &&
-        shard_len * c->k < 0x7FFFFFFFull)
+        shard_len * c->k < 0x7FFFFFFFull) {
         gs = spec_encoder(c, code_rb(rows));
-    if (!gs && jit_mode() == JIT_LOAD && c->m > 0 && c->k * c->m <= 16384)
-        return fail(HBRBC_E_INVALID_ARG, "HBRBC_JIT=load: %s", c->jit_missing.c_str());
+        // only a call the specialised encoder could serve fails on a missing
+        // code object; the others take the generic encoder below
+        if (!gs && jit_mode() == JIT_LOAD && c->k * c->m <= 16384)
+            return fail(HBRBC_E_INVALID_ARG, "HBRBC_JIT=load: %s", c->jit_missing.c_str());
+    }
     const char *fe = getenv("HBRBC_FUSE");   // 0: frame kernel + encoder (A/B)
     if (!gs || (fe && !std::strcmp(fe, "0"))) {
         st = frame_rows(c, payloads, payload_stride, payload_len, count, shards, shard_len, rows,

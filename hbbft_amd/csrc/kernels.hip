@@ -8,6 +8,7 @@
 //   Proof::validate    broadcast.rs:604-606, merkle.rs:83-103
 //   RS reconstruct     broadcast.rs:569 -> Coding::reconstruct_shards 682-693
 //   decode tail        broadcast.rs:580-600 (re-tree, root compare, unframe)
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -476,6 +477,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
 }
 
+// The same, two lanes per sponge (device_common.hpp keccak_f1600_pl), for
+// lists far below four waves per SIMD: validator-sharded cfg3 rebuilds 21 rows
+// of 4096 instances per step, 86,016 sponges = 1.3 waves per SIMD, where the
+// sponge's serial permutation chain -- not issue -- sets the time.
+__global__ __launch_bounds__(kBlock) void leaf_hash_list_pl_kernel(
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
+    const uint2 *__restrict__ list, const uint32_t *__restrict__ counter,
+    uint8_t *__restrict__ nodes, size_t node_inst_stride) {
+    const size_t g = (blockIdx.x * (size_t)kBlock + threadIdx.x) >> 1;
+    const uint32_t h = threadIdx.x & 1u;
+    if (g >= *counter) return;   // both lanes of a pair leave together
+    const uint2 e = list[g];
+    uint32_t d[8];
+    sha3_256_row_pl(shards + e.x * inst_stride + rows.off(e.y), S, h, d);
+    if (!h) store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
+}
+
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void ragged_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lens, size_t nvals, uint8_t *__restrict__ out) {
@@ -792,7 +810,8 @@ __global__ __launch_bounds__(kBlock) void pattern_lookup_kernel(
 // M[missing] * inv(M[valid]) (missing data rows are rows of the inverse;
 // missing parity rows equal rse's parity-from-rebuilt-data by linearity over
 // GF(2^8)), as coefficient bytes [pass][k][16] for gf_bitslice_kernel.
-// LDS: 1600 B of tables and lists + d x 2d + d x (k - d) <= 1600 + 3 k^2.
+// LDS: 1600 B of tables and lists + d x 2d + d x (k - d) = 1600 + d (d + k),
+// d <= min(k, n - k) (launch_decode_matrix sizes it for the largest d).
 __global__ __launch_bounds__(1024) void decode_matrix_kernel(
     int n, int k, int rt, const uint8_t *__restrict__ matrix, const uint8_t *__restrict__ present,
     PatternCache c, int *__restrict__ pat, const uint8_t *__restrict__ own) {
@@ -1294,6 +1313,21 @@ hipError_t launch_leaf_hash_rebuilt(const uint8_t *shards, size_t shard_len, con
     hipLaunchKernelGGL(rebuilt_list_kernel, dim3(grid_for(count, (size_t)1 << 30)), dim3(kBlock),
                        0, s, count, pat, out_idx, out_idx_stride, nout, counter, list);
     const size_t total = count * (size_t)max_rows;
+    // pair-lane sponges below HBRBC_LIST_PAIR_BELOW rows of the worst case
+    // (count x m; the list itself, count x missing rows, is known only on the
+    // device -- with f random erasures about half of it).  Default 2^18: the
+    // validator-sharded decodes (cfg3 4096 x 42, cfg4 2048 x 84 worst case,
+    // half of it listed) pair; the instance-mode leaf reuse (16384 x 42) not.
+    static const size_t pair_below = [] {
+        const char *e = getenv("HBRBC_LIST_PAIR_BELOW");
+        return e ? (size_t)atoll(e) : ((size_t)1 << 18);
+    }();
+    if (total < pair_below) {
+        hipLaunchKernelGGL(leaf_hash_list_pl_kernel, dim3(grid_for(2 * total, (size_t)1 << 30)),
+                           dim3(kBlock), 0, s, shards, (uint32_t)shard_len, rows, inst_stride,
+                           list, counter, nodes, node_inst_stride);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(leaf_hash_list_kernel, dim3(grid_for(total, (size_t)1 << 30)), dim3(kBlock),
                        0, s, shards, (uint32_t)shard_len, rows, inst_stride, list, counter, nodes,
                        node_inst_stride);
@@ -1372,7 +1406,10 @@ hipError_t launch_decode_matrix(const DecodeMatrixArgs &a, hipStream_t s) {
     for (int i = 0; i < 8; ++i) spec.mask[i] = a.spec_mask[i];
     hipLaunchKernelGGL(pattern_lookup_kernel, dim3(grid_for(a.count, (size_t)1 << 30)),
                        dim3(kBlock), 0, s, a.n, a.present, a.count, a.cache, a.pat, a.own, spec);
-    const size_t lds = 1600 + (size_t)a.k * 3 * a.k;
+    // d missing data rows, d <= min(k, m) (a pattern with more than m missing
+    // rows stops at TooFewShardsPresent before the solve)
+    const size_t dmax = (size_t)std::min(a.k, a.n - a.k);
+    const size_t lds = 1600 + dmax * (dmax + (size_t)a.k);
     // threads per instance by system size (measured per step, round 2, full
     // k x 2k inversion): k = 22 one wave, 0.46 -> 0.34 ms; k = 84 eight waves
     // (four: 1.60, eight: 1.19, sixteen: 1.23 ms).  Round 3 (d x d inversion,

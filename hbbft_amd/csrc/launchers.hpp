@@ -255,10 +255,21 @@ hipError_t configure_kernels();
 // u32[roots][W], full Echoes u32[W], counters u16[3][roots], flags u32, + 6 of
 // alignment slack for a block, rounded to 8; an instance's block holds its
 // hosted nodes' fields as structures of arrays.
-__host__ __device__ inline size_t sm_er_bytes(size_t n, size_t roots) { return roots == 1 ? n : 2 * n; }
+// Per-node state block of sim.hip (structure of arrays over an instance's
+// nodes).  Two or more roots: er u16[n] (echo entry | ready entry << 8),
+// cand u32[C][W], full u32[W], counters u16[3][C], flags u32.  One root (the
+// validator-sharded runs): the echo / ready entries of all senders as four
+// bitmasks u32x4[W] {EchoHash, full Echo, tampered full Echo, Ready} -- the
+// full-Echo mask is their .y -- then cand u32[W], counters u16[3], flags u32.
+// Rounded to 16 bytes (the one-root masks are read as 16-byte words).
+__host__ __device__ inline size_t sm_er_bytes(size_t n, size_t roots) {
+    return roots == 1 ? 16 * ((n + 31) / 32) : 2 * n;
+}
 __host__ __device__ inline size_t sm_state_bytes(size_t n, size_t roots) {
     const size_t w = (n + 31) / 32;
-    return (sm_er_bytes(n, roots) + 4 * roots * w + 4 * w + 6 * roots + 4 + 6 + 7) & ~(size_t)7;
+    const size_t full = roots == 1 ? 0 : 4 * w;
+    // (+ 6: the 4-byte alignment pads of cand and flags in a block)
+    return (sm_er_bytes(n, roots) + 4 * roots * w + full + 6 * roots + 4 + 6 + 15) & ~(size_t)15;
 }
 hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s);
 

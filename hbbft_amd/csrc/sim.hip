@@ -73,8 +73,11 @@ enum : uint32_t {
 // Per sender s a node keeps one 16-bit word (er[s]): bits 0..7 the echo
 // entry (EchoContent) -- 0 none, Hash: 0x10 | c, Full: 0x20 | t << 3 | c (a
 // stored full Echo is always proof index s, validate_proof checks it) -- and
-// bits 8..11 the Ready entry (root + 1, 0 none).  With one root (c = 0) the
-// entry fits a byte: echo in bits 0..5, Ready in bits 6..7 (Sm<true>).
+// bits 8..11 the Ready entry (root + 1, 0 none).  With one root (c = 0,
+// Sm<true>) an entry is three bits -- hash, full, tampered -- and the Ready
+// entry one: bit s of four masks {hash, full, tamper, ready} per 32 senders,
+// one 16-byte LDS word (N=128: 64 bytes per node instead of 128 + a 16-byte
+// full-Echo mask).
 __device__ __forceinline__ uint32_t enc_full(uint32_t c, uint32_t t) {
     return 0x20u | ((t & 1u) << 3) | (c & 7u);
 }
@@ -98,13 +101,13 @@ struct Sm {
     // state of (inst, me), structure of arrays over the instance's hosted
     // nodes (stride sd = nodes): the nodes of an instance are consecutive
     // threads, so every state access of a wave is one coalesced request
-    // [n][sd]: echo entry | ready entry << 8 (er16), or with one root (ONE:
-    // every root index is 0, so ready = 1) echo entry | ready << 6 in a byte
-    // (er8): half the LDS image, more resident workgroups
+    // [n][sd]: echo entry | ready entry << 8 (er16); with one root (ONE:
+    // every root index is 0, so ready = 1) [W][sd] masks {hash, full,
+    // tamper, ready} (em): a third of the LDS image, more resident workgroups
     uint16_t *er16;
-    uint8_t *er8;
+    uint4 *em;
     uint32_t *cand;           // [C][W][sd]
-    uint32_t *full;           // [W][sd]: senders whose entry is a full Echo
+    uint32_t *full;           // [W][sd]: senders whose entry is a full Echo (ONE: em .y)
     uint16_t *cnt;            // [3][C][sd]: Echo+EchoHash, full Echo, Ready counts
     uint32_t *flags;          // [sd]
     size_t sd;
@@ -112,33 +115,47 @@ struct Sm {
     const uint8_t *dok;       // this instance's decode_ok [C]
 
     __device__ uint32_t ECHO(int s) const {
-        if constexpr (ONE) return er8[(size_t)s * sd] & 0x3Fu;
-        else return er16[(size_t)s * sd] & 0xFFu;
+        if constexpr (ONE) {
+            const uint4 v = em[(size_t)(s >> 5) * sd];
+            const uint32_t b = 1u << (s & 31);
+            return (v.y & b) ? (0x20u | ((v.z & b) ? 8u : 0u)) : ((v.x & b) ? 0x10u : 0u);
+        } else {
+            return er16[(size_t)s * sd] & 0xFFu;
+        }
     }
     __device__ void set_echo(int s, uint32_t e) {
         if constexpr (ONE) {
-            uint8_t &b = er8[(size_t)s * sd];
-            b = (uint8_t)((b & 0xC0u) | e);
+            uint4 &v = em[(size_t)(s >> 5) * sd];
+            const uint32_t b = 1u << (s & 31);
+            uint4 t = v;
+            t.x = (e & 0x10u) ? (t.x | b) : (t.x & ~b);
+            t.y = (e & 0x20u) ? (t.y | b) : (t.y & ~b);
+            t.z = (e & 0x28u) == 0x28u ? (t.z | b) : (t.z & ~b);
+            v = t;
         } else {
             uint16_t &w = er16[(size_t)s * sd];
             w = (uint16_t)((w & 0xFF00u) | e);
         }
     }
     __device__ uint32_t READY(int s) const {
-        if constexpr (ONE) return er8[(size_t)s * sd] >> 6;
+        if constexpr (ONE) return (em[(size_t)(s >> 5) * sd].w >> (s & 31)) & 1u;
         else return er16[(size_t)s * sd] >> 8;
     }
     __device__ void set_ready(int s, uint32_t r) {
         if constexpr (ONE) {
-            uint8_t &b = er8[(size_t)s * sd];
-            b = (uint8_t)((b & 0x3Fu) | (r << 6));
+            uint32_t &m = reinterpret_cast<uint32_t *>(&em[(size_t)(s >> 5) * sd])[3];
+            const uint32_t b = 1u << (s & 31);
+            m = r ? (m | b) : (m & ~b);
         } else {
             uint16_t &w = er16[(size_t)s * sd];
             w = (uint16_t)((w & 0xFFu) | (r << 8));
         }
     }
     __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
-    __device__ uint32_t &FULL(int w) { return full[(size_t)w * sd]; }
+    __device__ uint32_t &FULL(int w) {
+        if constexpr (ONE) return reinterpret_cast<uint32_t *>(&em[(size_t)w * sd])[1];
+        else return full[(size_t)w * sd];
+    }
     uint16_t r_ce = 0, r_cf = 0, r_cr = 0;
     uint32_t r_flags = 0;
     __device__ uint16_t &CE(uint32_t c) {
@@ -308,8 +325,8 @@ struct Sm {
         }
         if (!e) ++CE(c);   // a Hash of the same root was counted already
         ++CF(c);
-        set_echo(s, enc_full(c, t));
-        FULL(s >> 5) |= 1u << (s & 31);
+        set_echo(s, enc_full(c, t));   // (ONE: sets the full-Echo bit too)
+        if constexpr (!ONE) FULL(s >> 5) |= 1u << (s & 31);
         if (!(FLAGS() & (1u << (FL_CAN_DECODE_SHIFT + c))) && CF(c) >= k) send_can_decode(c);
         if (!(FLAGS() & FL_READY_SENT) && CE(c) >= n - f) send_ready(c);
         if (FLAGS() & FL_READY_SENT) compute_output(c);
@@ -448,16 +465,16 @@ __device__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {  
 
 
 // Byte offsets of the fields of an instance's state block holding `sd` nodes
-// as structures of arrays (include/hbrbc.h hbrbc_sm_state_bytes, per node:
-// er u16[n] (u8[n] with one root), cand u32[C][W], full u32[W], counters
-// u16[3][C], flags u32).
+// as structures of arrays (launchers.hpp sm_state_bytes, per node: er u16[n]
+// or, with one root, masks u32x4[W]; cand u32[C][W]; full u32[W] (not with
+// one root); counters u16[3][C]; flags u32).
 struct SmLayout {
     size_t er, cand, full, cnt, flags;
     __device__ SmLayout(int n, int C, int W, size_t sd) {
         er = 0;
         cand = (sm_er_bytes((size_t)n, (size_t)C) * sd + 3) & ~(size_t)3;
         full = cand + 4 * (size_t)C * W * sd;
-        cnt = full + 4 * (size_t)W * sd;
+        cnt = full + (C == 1 ? 0 : 4 * (size_t)W * sd);
         flags = (cnt + 6 * (size_t)C * sd + 3) & ~(size_t)3;
     }
 };
@@ -486,7 +503,7 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
     m.role = a.role[inst * n + me];
     m.sd = sd;
     m.er16 = reinterpret_cast<uint16_t *>(st + L.er) + local;
-    m.er8 = st + L.er + local;
+    m.em = reinterpret_cast<uint4 *>(st + L.er) + local;
     m.cand = reinterpret_cast<uint32_t *>(st + L.cand) + local;
     m.full = reinterpret_cast<uint32_t *>(st + L.full) + local;
     m.cnt = reinterpret_cast<uint16_t *>(st + L.cnt) + local;

@@ -59,6 +59,18 @@ class SmArgs(ctypes.Structure):
             "state", "output_root", "faults", "fault_count", "emitted")]
 
 
+def sm_state_bytes_host(n, roots):
+    """hbrbc_sm_state_bytes without the library (hbbft_amd/csrc/launchers.hpp
+    sm_state_bytes): per node, with several roots a u16 echo/ready entry per
+    sender, can_decode masks per root, a full-Echo mask; with one root four
+    bitmasks per 32 senders and the can_decode mask; counters and flags;
+    rounded to 16 bytes."""
+    w = (n + 31) // 32
+    er = 16 * w if roots == 1 else 2 * n
+    full = 0 if roots == 1 else 4 * w
+    return (er + 4 * roots * w + full + 6 * roots + 4 + 6 + 15) & ~15
+
+
 def _bind():
     L = lib()
     if not getattr(L, "_sm_bound", False):
@@ -197,6 +209,13 @@ class StateMachineRank:
         self.n, self.count, self.roots = n, count, roots
         self.rank, self.world = rank, world
         self.R = -(-n // world)
+        # every rank hosts at least one node (sharded.Topology's rule): with
+        # n=10, world=8 ranks 5..7 would start at node 10..14
+        if world < 1 or (world - 1) * self.R >= n:
+            raise ValueError("world %d leaves rank %d without nodes at n=%d"
+                             % (world, world - 1, n))
+        if not 0 <= rank < world:
+            raise ValueError("rank %d outside world %d" % (rank, world))
         self.node_lo = rank * self.R
         self.W = (n + 31) // 32
         self.rec = 1 + self.W

@@ -481,6 +481,98 @@ class ShardedBroadcast:
         }
 
 
+HBM_PER_GPU = 288 * 10**9   # MI355X HBM3E
+
+
+def rank_footprint(n, count, plen, world, rank=0, max_out=4, max_faults=4):
+    """Device bytes one rank's ShardedBroadcast(n, count, plen, rank, world)
+    allocates, by buffer, without a GPU: the torch tensors of __init__ (and
+    of its StateMachineRank) at their exact shapes, aliases at world 1
+    counted once, plus an upper bound of the library's reconstruct workspace
+    (hbrbc_reserve: decode-matrix cache of cap + count slots, coefficient
+    rows at one row per pass).  tests/test_sharded.py checks the torch part
+    against torch.cuda.memory_allocated on the GPU."""
+    from . import max_proof_len, merkle_node_count
+    t = Topology(n, world)
+    f = t.f
+    k = n - 2 * f
+    S = shard_len(plen, k)
+    stride = (S + 15) // 16 * 16
+    ds = max(max_proof_len(n), 1)
+    dsz = ds * 32 + 16
+    G, R, C = world, t.rpg, count
+    nc = merkle_node_count(n)
+    vreal = len(t.validators(rank))
+    echo = t.echo_rows(rank) if G > 1 else []
+    own = [j for j in t.validators(rank) if t.receiver_present(rank)[j]]
+    W = (n + 31) // 32
+    sm_state = _sm_state_bytes(n, 1)
+    b = {
+        "slab": G * C * R * stride,
+        "nodes": C * nc * 32,
+        "digests": C * n * ds * 32,
+        "ndig": C * n,
+        "dg_flat": C * t.npad * dsz,
+        "send_dg": G * C * R * dsz,
+        "roots_all": G * C * 32,
+        "vrows_t": vreal * 4,
+        "recv_idx": G * C * vreal * 4,
+        "ok_v": G * C * vreal,
+        "ok_pad": G * C * R,
+        "v_digests": G * C * R * ds * 32,
+        "v_ndig": G * C * R,
+        "echo_rows_t": max(1, len(echo)) * 4,
+        "ok_e": G * C * max(1, len(echo)),
+        "present": G * C * n,
+        "dec_nodes": G * C * nc * 32,
+        "out": G * C * max(16, (k * S + 15) // 16 * 16),
+        "plen_out": G * C * 4,
+        "status": G * C * 4,
+        "echo_senders": G * C * 4,
+        "full_echos": G * C * 4,
+        "decided": G * C,
+        "sm_ok": G * C * 2 * n,
+        "sm_dec": G * C,
+        "own_cols": max(1, len(own)) * 8,
+        "own_rows": max(1, len(own)) * 8,
+        "echo_cols": max(1, len(echo)) * 8,
+        # StateMachineRank (rbc_sim.py) of G * C instances, honest scenario
+        "sm_scenario": G * C * (1 + 3 * n + 2) + G * C * W * 4,
+        "sm_state": G * C * R * sm_state,
+        "sm_out": G * C * R * max_out * (1 + W) * 4,
+        "sm_out_count": G * C * R * 4,
+        "sm_output_root": G * C * R,
+        "sm_faults": G * C * R * max(1, max_faults) * 2,
+        "sm_fault_count": G * C * R * 4,
+        "sm_emitted": 8,
+        "sm_inbox": G * G * C * R * max_out * (1 + W) * 4,
+        "sm_inbox_count": G * G * C * R * 4,
+    }
+    if G > 1:
+        b.update({"recv_sh": G * C * R * stride, "recv_dg": G * C * R * dsz,
+                  "okv_all": G * G * C * R, "echo_sh": G * G * C * R * stride,
+                  "echo_dg": G * G * C * R * dsz, "e_digests": G * C * t.npad * ds * 32,
+                  "e_ndig": G * C * t.npad})
+    inst = G * C
+    cap = 1024
+    while cap < 2 * inst:
+        cap *= 2
+    slots = cap + inst
+    lib_ws = (cap * 8 + slots * (32 + (2 * f * k * 16 + 16) + 4 * (k + 2 * f) + 8)
+              + inst * (4 + 1 + 4) + (inst * max(2 * f, 1) + 1) * 8)
+    torch_bytes = sum(b.values())
+    return {"buffers": b, "torch_bytes": torch_bytes, "library_workspace_bound": lib_ws,
+            "total_bytes": torch_bytes + lib_ws, "hbm_bytes": HBM_PER_GPU,
+            "frac_of_hbm": (torch_bytes + lib_ws) / HBM_PER_GPU}
+
+
+def _sm_state_bytes(n, roots):
+    """hbrbc_sm_state_bytes (include/hbrbc.h) without loading the library:
+    the per-node state block of sim.hip, 8-byte aligned."""
+    from .rbc_sim import sm_state_bytes_host
+    return sm_state_bytes_host(n, roots)
+
+
 def pipelined_step(subs, payloads, ex, timer):
     """One step over several sub-batches (ShardedBroadcast objects on the same
     rank, payloads[i] for subs[i]) with every exchange in flight on the

@@ -86,16 +86,20 @@ def test_no_cpu_fallback_without_gpu():
 
 def test_state_machine_block_size():
     """hbrbc_sm_state_bytes (include/hbrbc.h): per node, the echo/ready entry
-    of every sender (one byte with one root, two otherwise), can_decode and
-    full-Echo masks, counters and flags, rounded to 8 bytes."""
-    import hbbft_amd.rbc_sim  # noqa: F401  (declares the restype)
+    of every sender (two bytes per sender with several roots; with one root
+    four 32-sender bitmasks -- hash, full, tampered, ready -- per 32 senders),
+    can_decode and (several roots) full-Echo masks, counters and flags,
+    rounded to 16 bytes; rbc_sim.sm_state_bytes_host mirrors it."""
+    from hbbft_amd.rbc_sim import sm_state_bytes_host
     L = hb.lib()
     L.hbrbc_sm_state_bytes.restype = ctypes.c_size_t
     L.hbrbc_sm_state_bytes.argtypes = [ctypes.c_size_t, ctypes.c_size_t]
     for n in (1, 4, 16, 31, 64, 128, 250):
         w = (n + 31) // 32
         for roots in (1, 2, 3):
-            er = n if roots == 1 else 2 * n
-            want = (er + 4 * roots * w + 4 * w + 6 * roots + 4 + 6 + 7) & ~7
+            er = 16 * w if roots == 1 else 2 * n
+            full = 0 if roots == 1 else 4 * w
+            want = (er + 4 * roots * w + full + 6 * roots + 4 + 6 + 15) & ~15
             got = L.hbrbc_sm_state_bytes(n, roots)
-            assert got == want and got % 8 == 0, (n, roots, got, want)
+            assert got == want and got % 16 == 0, (n, roots, got, want)
+            assert sm_state_bytes_host(n, roots) == got

@@ -103,6 +103,54 @@ def make_instances(n, rng, seed_tag=0):
     return out
 
 
+SINGLE_KINDS = ("honest", "silent", "corrupt_echo", "withhold_echo", "partial_values",
+                "tampered_values", "faulty_mix")
+
+
+def make_single_root_instances(n, rng, seed_tag=0):
+    """Scenario instances with ONE codeword each (Scenario.roots == 1), the
+    form the validator-sharded runs use (sim.hip Sm<true>: one-byte Echo /
+    Ready entries, counters and flags in registers): every adversary that
+    needs no second value -- silent faulty nodes (the ProposeAdversary's drop
+    without its injected broadcasts), corrupted or withheld Echoes, a faulty
+    proposer that sends nothing or tampered proofs to some validators, and a
+    mixture of those."""
+    f = vn.max_faulty(n)
+    out = []
+    for kind in SINGLE_KINDS:
+        bad_proposer = kind in ("partial_values", "tampered_values", "faulty_mix") and f > 0
+        p = rng.randrange(f) if bad_proposer else rng.randrange(n)
+        val = b"S-%d-%d-%s-" % (n, seed_tag, kind.encode()) + bytes(
+            rng.randrange(256) for _ in range(rng.randrange(0, 64)))
+        role = [HONEST] * n
+        vr, vt = [0] * n, [0] * n
+        if kind == "silent":
+            for F in _faulty(n):
+                role[F] = SILENT
+        elif kind == "corrupt_echo":
+            for F in _faulty(n):
+                role[F] = CORRUPT_ECHO
+        elif kind == "withhold_echo":
+            for F in _faulty(n):
+                role[F] = WITHHOLD_ECHO
+        elif kind == "partial_values" and f:
+            for j in rng.sample(range(n), min(n - 1, f + 1)):
+                if j != p:
+                    vr[j] = NONE
+        elif kind == "tampered_values" and f:
+            for j in rng.sample(range(n), min(n, f + 1)):
+                vt[j] = 1
+        elif kind == "faulty_mix" and f:
+            for j in range(n):
+                vr[j] = rng.choice([0, 0, 0, 0, NONE])
+                vt[j] = 1 if rng.random() < 0.15 else 0
+            vr[p], vt[p] = 0, 0
+            for F in _faulty(n):
+                role[F] = rng.choice([HONEST, SILENT, CORRUPT_ECHO, WITHHOLD_ECHO])
+        out.append(Instance(n, p, [val], vr, vt, role))
+    return out
+
+
 def host_run(inst):
     outs, faults, rounds = vn.run_rounds(inst, _oracle())
     return outs, faults, rounds
@@ -209,6 +257,68 @@ def test_state_machine_matches_host_restatement(n, worlds):
                 got = [] if outs[(i, node)] is None else [outs[(i, node)]]
                 assert got == ho[node], (world, i, node, got, ho[node])
                 assert faults[(i, node)] == hf[node], (world, i, node, faults[(i, node)], hf[node])
+
+
+_HOST_CACHE = {}
+
+
+def _single_root_case(n):
+    """The single-root scenario of validator count n and its host results
+    (computed once per n for all kernel forms and worlds)."""
+    if n not in _HOST_CACHE:
+        rng = random.Random(5000 + n)
+        insts = make_single_root_instances(n, rng) + make_single_root_instances(n, rng, 1)
+        scn = Scenario(n, insts)
+        assert scn.roots == 1
+        _HOST_CACHE[n] = (scn, [host_run(inst) for inst in insts])
+    return _HOST_CACHE[n]
+
+
+# the launch forms of hbrbc_sm_round (sim.hip launch_sm_round): the staged
+# kernel at 4 waves/SIMD (128 VGPRs, spills) and at the default budget, and the
+# global form; max_out 8 keeps the N=128 staged image under 64 KiB
+SM_FORMS = {"staged_w4": {"HBRBC_SM_W4": "1"}, "staged_w3": {"HBRBC_SM_W4": "0"},
+            "global": {"HBRBC_SM_STAGED": "0"}}
+
+
+def test_single_root_scenarios_on_host():
+    """CPU: the single-root scenarios are well formed (one root) and the host
+    restatement keeps the reference's guarantees on them."""
+    rng = random.Random(11)
+    for n in (4, 7, 16):
+        f = vn.max_faulty(n)
+        insts = make_single_root_instances(n, rng)
+        assert Scenario(n, insts).roots == 1
+        for inst in insts:
+            outs, faults, _ = host_run(inst)
+            correct = [outs[i] for i in range(f, n)]
+            assert len({tuple(o) for o in correct}) == 1
+            for i in range(f, n):
+                assert all(b < f or b == inst.proposer for b, _ in faults[i]), (i, faults[i])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", sorted(SM_FORMS))
+@pytest.mark.parametrize("n", [4, 16, 64, 128])
+def test_single_root_state_machine_matches_host(n, form, monkeypatch):
+    """The one-root kernels (Sm<true>) the validator-sharded bench runs, in
+    each launch form, per node against the host restatement: outputs, fault
+    logs (blamed node + kind, in order) and round count, over worlds 1, 2, 8
+    (the worlds that leave every rank a node)."""
+    from hbbft_amd.rbc_sim import simulate
+    for k, v in SM_FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    scn, ref = _single_root_case(n)
+    worlds = [w for w in (1, 2, 8) if (w - 1) * -(-n // w) < n]
+    for world in worlds:
+        outs, faults, rounds = simulate(scn, world=world, max_out=8)
+        assert rounds == max(r[2] for r in ref), (world, rounds, [r[2] for r in ref])
+        for i, (ho, hf, _) in enumerate(ref):
+            for node in range(n):
+                got = [] if outs[(i, node)] is None else [outs[(i, node)]]
+                assert got == ho[node], (form, world, i, node, got, ho[node])
+                assert faults[(i, node)] == hf[node], (form, world, i, node, faults[(i, node)],
+                                                       hf[node])
 
 
 @pytest.mark.gpu

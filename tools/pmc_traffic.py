@@ -9,8 +9,8 @@ of a wide streaming read, so it is doubled.  Output (out.json): bytes per
 launch and per instance for every hbrbc kernel of every profiled config, and
 the "cfg:stage" -> bytes-per-instance map bench.py reads for roofline.traffic.
 With an SQ pass and a sponge geometry it also writes
-profiles/valu_ops_per_perm.json: 32-bit lane-ops per Keccak-f[1600] of the
-leaf-hash kernel = SQ_INSTS_VALU x 64 / permutations per launch.
+profiles/valu_ops_per_perm.json[config]: 32-bit lane-ops per Keccak-f[1600] of
+the leaf-hash kernel = SQ_INSTS_VALU x 64 / permutations per launch.
 
 usage: pmc_traffic.py <out.json> <profile dir>:<config>:<instances per launch>
                       [:<n>:<shard_len>] ...
@@ -90,11 +90,20 @@ def main():
             if leaf:
                 perms = inst * n * ((S + 1 + 135) // 136)
                 ops = leaf[0] * 64.0 / perms
-                json.dump({"leaf_hash_kernel": ops, "source": "%s, %s: SQ_INSTS_VALU %.0f x 64 / "
-                           "%d permutations per launch" % (os.path.basename(d), cfg, leaf[0], perms)},
-                          open(os.path.join(os.path.dirname(out), "valu_ops_per_perm.json"), "w"),
-                          indent=1)
-                print("leaf_hash lane-ops per permutation: %.1f" % ops)
+                # keyed by config: the bench line of config c uses c's own pass
+                vp = os.path.join(os.path.dirname(out), "valu_ops_per_perm.json")
+                try:
+                    vdoc = json.load(open(vp))
+                except (OSError, ValueError):
+                    vdoc = {}
+                if "leaf_hash_kernel" in vdoc:   # the round-3 flat form
+                    vdoc = {}
+                vdoc[cfg] = {"leaf_hash_kernel": ops, "sq_insts_valu_per_launch": leaf[0],
+                             "perms_per_launch": perms,
+                             "source": "%s, %s: SQ_INSTS_VALU %.0f x 64 / %d permutations per "
+                                       "launch" % (os.path.basename(d), cfg, leaf[0], perms)}
+                json.dump(vdoc, open(vp, "w"), indent=1, sort_keys=True)
+                print("%s leaf_hash lane-ops per permutation: %.1f" % (cfg, ops))
     traffic["_note"] = ("HBM bytes per instance per launch: (2 x FETCH_SIZE + WRITE_SIZE) x 1024 "
                         "/ instances per launch (rocprofv3 --pmc passes, tools/profile.sh)")
     json.dump({"kernels": kernels_all, "traffic": traffic}, open(out, "w"), indent=1)

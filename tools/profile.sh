@@ -9,7 +9,7 @@ TAG=${TAG:-r2}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 ARGS=${BENCH_ARGS:---steps 5 --warmup 1 --no-cpu --mode instances}
-PARGS=${PMC_ARGS:---steps 1 --warmup 1 --no-cpu --mode instances --no-verify}
+PARGS=${PMC_ARGS:---steps 1 --warmup 1 --no-cpu --mode instances --no-verify --no-leaf-reuse}
 fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $ROOT/bench.py $ARGS > $OUT/trace.log 2>&1
 rc=$?; echo "trace exit $rc"; tail -c 1500 $OUT/trace.log; echo
