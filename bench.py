@@ -242,11 +242,39 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
                   "perms_per_launch": perms[dom], "perms_per_s": pps,
                   "ops_per_perm": opp, "ops_per_perm_source": src,
                   "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
-                  "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS})
+                  "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS,
+                  "profiled": profiled_frac(config, perms[dom], opp)})
     else:
         r.update({"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": hbm_gbs / HBM_PEAK_GBS})
     return r
+
+
+def profiled_frac(config, perms_per_launch, opp):
+    """The same roofline from committed files only: the dominant kernel's
+    average duration in the rocprofv3 --kernel-trace --stats summary named by
+    profiles/roofline_sources.json[config], and the SQ_INSTS_VALU counter of
+    profiles/valu_ops_per_perm.json[config] -- so `frac` can be recomputed
+    from profiles/ (the live `frac` above uses this run's HIP events)."""
+    import csv
+    try:
+        src = json.load(open(os.path.join(ROOT, "profiles", "roofline_sources.json")))[config]
+        path = os.path.join(ROOT, src["kernel_stats"])
+        avg_ns = None
+        for row in csv.DictReader(open(path)):
+            if src["kernel"] in row["Name"]:
+                avg_ns = float(row["AverageNs"])
+                break
+        if avg_ns is None:
+            return None
+    except (OSError, ValueError, KeyError):
+        return None
+    pps = perms_per_launch / (avg_ns * 1e-9)
+    return {"kernel_stats": src["kernel_stats"], "kernel": src["kernel"],
+            "avg_ms": avg_ns / 1e6, "perms_per_s": pps, "ops_per_perm": opp,
+            "lane_ops_per_s": pps * opp, "frac": pps * opp / VALU_PEAK_OPS,
+            "note": "valid when this line's instances per launch equal the profiled run's (%s)"
+                    % src.get("instances", "?")}
 
 
 def valu_ops_per_perm(config):
@@ -653,7 +681,11 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                                   world),
                    "proposals_per_gpu": count, "instances_per_step": count * world,
                    "parallelism": "validator-sharded x%d" % world,
-                   "pipelined_sub_batches": nsub},
+                   "pipelined_sub_batches": nsub,
+                   # per-rank device bytes of this object at 1/2/4/8 GPUs (rank 0;
+                   # hbbft_amd.sharded.rank_footprint, torch buffers + reconstruct
+                   # workspace bound), against 288 GB of HBM per MI355X
+                   "hbm_footprint_per_rank": footprint_summary(n, count, plen)},
         "exchange": {"ms_per_step": xms, "bytes_per_step_per_gpu": xbytes,
                      "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
                      "backend": ex.backend, "per_rank": per_rank},
@@ -661,6 +693,17 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         "stages_ms_per_step": dict({s: stages[s][0] / args.steps for s in stages},
                                    state_machine=sm_ms),
     }
+
+
+def footprint_summary(n, count, plen):
+    from hbbft_amd.sharded import HBM_PER_GPU, rank_footprint
+    out = {}
+    for g in (1, 2, 4, 8):
+        fp = rank_footprint(n, count, plen, g, 0)
+        out["G%d" % g] = {"bytes": fp["total_bytes"], "frac_of_288GB": fp["frac_of_hbm"],
+                          "echo_slab_bytes": fp["buffers"].get("echo_sh", fp["buffers"]["slab"])}
+    assert all(v["bytes"] < HBM_PER_GPU for v in out.values()), out
+    return out
 
 
 # --------------------------------------------------------------------- main --

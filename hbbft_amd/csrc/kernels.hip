@@ -297,15 +297,16 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
         const uint4 *cfp = reinterpret_cast<const uint4 *>(cf) + (size_t)p * nin;
         // Loads are unconditional (index clamped, a half chunk re-reads its own
         // 16 bytes) so hipcc can count vmcnt exactly instead of draining.
-        auto load_in = [&](int jj, uint4 &l, uint4 &h) {
-            const uint8_t *src = ib + rows.off(iidx[jj < nin ? jj : nin - 1]) + off;
+        auto row_of = [&](int jj) { return iidx[jj < nin ? jj : nin - 1]; };
+        auto coef_of = [&](int jj) { return cfp[jj < nin ? jj : nin - 1]; };
+        auto load_row = [&](uint32_t r, uint4 &l, uint4 &h) {
+            const uint8_t *src = ib + rows.off(r) + off;
             l = *reinterpret_cast<const uint4 *>(src);
             h = *reinterpret_cast<const uint4 *>(src + d2);
         };
-        auto consume = [&](int jj, const uint4 &lo, const uint4 &h) {
+        auto consume = [&](uint32_t r, const uint4 &cw, const uint4 &lo, const uint4 &h) {
             const uint4 hi = full ? h : make_uint4(0, 0, 0, 0);
             if (ufp && p == 0) {
-                const uint32_t r = iidx[jj];
                 if (r < uf_k && active) {
                     unframe_put(ufp, uf_S, r, off, lo.x, lo.y, lo.z, lo.w);
                     if (full) unframe_put(ufp, uf_S, r, off + d2, hi.x, hi.y, hi.z, hi.w);
@@ -313,8 +314,7 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
             }
             uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
             bs_transpose(x);
-            // RT coefficient bytes of input jj for this pass (16-byte padded, scalar load)
-            const uint4 cw = cfp[jj];
+            // RT coefficient bytes of this input for this pass (16-byte padded)
             const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
             // At step b the planes of 2^b * x sit rotated: logical plane q is
             // x[(q - b) & 7], so doubling moves no registers, only XORs h into
@@ -343,20 +343,45 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
                 }
             }
         };
+        // Software pipeline, unrolled by two so no register ever moves: the 32
+        // input bytes of j+1 are in flight (buffer B) while input j (buffer A)
+        // is consumed, and vice versa.  The scalar operands run one input
+        // further ahead: the row index of the next load and the coefficients
+        // of the next input are requested before this input's XOR work and
+        // waited for after it.  (Scalar loads return out of order, so any
+        // wait is lgkmcnt(0): the empty asm forces that wait at the top of a
+        // half-step, before the next requests go out -- round 3 waited on
+        // each index and coefficient load right where it was issued, an L2
+        // round trip per input.)
+        uint32_t ra = row_of(0), rb = row_of(1);
+        uint4 cwa = coef_of(0), cwb;
+        // the pass's output rows, requested with the first operands (the
+        // stores below would otherwise wait on one scalar load per row)
+        uint32_t orows[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) orows[t] = oidx[p * RT + t < nout ? p * RT + t : nout - 1];
         uint4 alo, ahi, blo = make_uint4(0, 0, 0, 0), bhi = make_uint4(0, 0, 0, 0);
-        load_in(0, alo, ahi);
+        load_row(ra, alo, ahi);
         for (int j = 0; j < nin; j += 2) {
-            load_in(j + 1, blo, bhi);
-            consume(j, alo, ahi);
-            load_in(j + 2, alo, ahi);
-            if (j + 1 < nin) consume(j + 1, blo, bhi);
+            __asm__ volatile("" ::"s"(rb), "s"(cwa.x), "s"(cwa.y), "s"(cwa.z), "s"(cwa.w) : "memory");
+            load_row(rb, blo, bhi);
+            const uint32_t rn = row_of(j + 2);
+            cwb = coef_of(j + 1);
+            consume(ra, cwa, alo, ahi);
+            __asm__ volatile("" ::"s"(rn), "s"(cwb.x), "s"(cwb.y), "s"(cwb.z), "s"(cwb.w) : "memory");
+            load_row(rn, alo, ahi);
+            const uint32_t rn2 = row_of(j + 3);
+            cwa = coef_of(j + 2);
+            if (j + 1 < nin) consume(rb, cwb, blo, bhi);
+            ra = rn;
+            rb = rn2;
         }
         if (active) {
 #pragma unroll
             for (int t = 0; t < RT; ++t) {
                 if (p * RT + t < nout) {
                     bs_transpose(acc[t]);
-                    const uint32_t orow = oidx[p * RT + t];
+                    const uint32_t orow = orows[t];
                     uint8_t *dst = ib + rows.off(orow) + off;
                     store16_stream(dst, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
                     if (full) store16_stream(dst + d2, acc[t][4], acc[t][5], acc[t][6], acc[t][7]);

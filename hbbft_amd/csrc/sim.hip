@@ -566,6 +566,7 @@ __device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t ins
 // does not fit the LDS budget (sm_plan).
 template <bool ONE>
 __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, int f, int k) {
+    if (a.active && *a.active == 0u) return;   // quiescent: nothing was sent last round
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (g >= a.count * a.nodes) return;
     const size_t inst = g / a.nodes;
@@ -593,6 +594,7 @@ template <bool ONE>
 __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, int f, int k,
                                                 int ipb) {
     extern __shared__ uint4 sm_lds4[];
+    if (a.active && *a.active == 0u) return;   // quiescent (uniform: the whole block leaves)
     uint8_t *lds = reinterpret_cast<uint8_t *>(sm_lds4);
     const int T = (int)blockDim.x, tid = (int)threadIdx.x;
     const size_t inst0 = (size_t)blockIdx.x * ipb;

@@ -56,7 +56,7 @@ class SmArgs(ctypes.Structure):
         (name, _P) for name in (
             "proposer", "role", "value_root", "value_tamper", "proof_ok", "decode_ok",
             "fake_from", "fake_root", "fake_list", "in_", "in_count", "out", "out_count",
-            "state", "output_root", "faults", "fault_count", "emitted")]
+            "state", "output_root", "faults", "fault_count", "emitted", "active")]
 
 
 def sm_state_bytes_host(n, roots):
@@ -205,7 +205,7 @@ class StateMachineRank:
     proof_ok [count][roots][2][n] and decode_ok [count][roots]."""
 
     def __init__(self, n, count, roots, sc, rank, world, device=0, max_out=24, max_faults=32,
-                 ok=None, dec=None):
+                 ok=None, dec=None, max_rounds=64):
         self.n, self.count, self.roots = n, count, roots
         self.rank, self.world = rank, world
         self.R = -(-n // world)
@@ -234,7 +234,9 @@ class StateMachineRank:
         self.output_root = torch.full((cnt, R), NONE, dtype=torch.uint8, device=dev)
         self.faults = torch.zeros((cnt, R, max(1, max_faults)), dtype=torch.int16, device=dev)
         self.fault_count = torch.zeros((cnt, R), dtype=torch.int32, device=dev)
-        self.emitted = torch.zeros(2, dtype=torch.int32, device=dev)   # records, overflow flag
+        # per round: records emitted, overflow flag (hbrbc_sm_args.emitted of round r)
+        self.max_rounds = max_rounds
+        self.hist = torch.zeros((max_rounds, 2), dtype=torch.int32, device=dev)
         # every sender's records of the previous round, [G][count][R][E][rec]
         self.inbox = torch.zeros((world, cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
         self.inbox_count = torch.zeros((world, cnt, R), dtype=torch.int32, device=dev)
@@ -250,6 +252,7 @@ class StateMachineRank:
     def reset(self):
         """Fresh nodes (before round 0 of another run)."""
         self.state.zero_()
+        self.hist.zero_()
         self.out_count.zero_()
         self.inbox_count.zero_()
         self.output_root.fill_(NONE)
@@ -261,8 +264,13 @@ class StateMachineRank:
         self.inbox, self.out = self.out.unsqueeze(0), self.inbox[0]
         self.inbox_count, self.out_count = self.out_count.unsqueeze(0), self.inbox_count[0]
 
-    def round(self, r, stream=None):
-        """Handle round r's inbox (round 0: the proposers' broadcast())."""
+    def round(self, r, active=None, stream=None):
+        """Handle round r's inbox (round 0: the proposers' broadcast()).
+        active: None, or a device int32 scalar tensor -- the records every
+        sender emitted in round r - 1; the kernel returns at once when it is
+        0 (quiescent), so rounds can be enqueued without reading back."""
+        if r >= self.max_rounds:
+            raise RuntimeError("state machine: round %d past max_rounds %d" % (r, self.max_rounds))
         s = self.sc
         a = SmArgs(count=self.count, node_lo=self.node_lo, nodes=self.R, rows_per_rank=self.R,
                    roots=self.roots, max_out=self.max_out, max_faults=self.max_faults, round=r)
@@ -274,20 +282,15 @@ class StateMachineRank:
         a.out, a.out_count = self.out.data_ptr(), self.out_count.data_ptr()
         a.state, a.output_root = self.state.data_ptr(), self.output_root.data_ptr()
         a.faults, a.fault_count = self.faults.data_ptr(), self.fault_count.data_ptr()
-        a.emitted = self.emitted.data_ptr()
-        self.emitted.zero_()
+        a.emitted = self.hist[r].data_ptr()
+        a.active = None if active is None else active.data_ptr()
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(_bind().hbrbc_sm_round(self.rb.coding.handle, ctypes.byref(a),
                                       ctypes.c_void_p(st.cuda_stream)))
 
-    def poll(self):
-        """Records emitted in the last round (one device-to-host read); raises
-        if a node emitted more than max_out (out_count bit 31)."""
-        e = self.emitted.cpu()
-        if int(e[1]):
-            raise RuntimeError("state machine: a node emitted more than %d messages in a round"
-                               % self.max_out)
-        return int(e[0])
+    def emitted(self, r):
+        """Device int32 scalar: records this rank emitted in round r."""
+        return self.hist[r, 0]
 
     def exchange(self, ex, async_op=False):
         """All-gather of this round's records (the Ready / EchoHash / CanDecode
@@ -331,70 +334,116 @@ class LoopbackExchange:
             r.inbox_count.copy_(cnts)
 
 
+ROUND_BATCH = 6   # rounds enqueued per read-back (honest runs quiesce after 5)
+
+
+def _check_batch(ranks, h, r0, own=None):
+    """h [ranks][rounds][2] (host) of rounds r0..: records per round and the
+    overflow flags; returns the number of rounds run if one of them was
+    quiescent (no records anywhere), else None.  own: the records of THIS
+    rank per (sub-batch, round) where h holds every rank's totals."""
+    for i in range(h.shape[1]):
+        if int(h[:, i, 1].max()):
+            raise RuntimeError("state machine: a node emitted more than %d messages in a round"
+                               % ranks[0].max_out)
+        mine = h[:, i, 0] if own is None else own[:, i]
+        for sm, c in zip(ranks, mine):
+            sm.records += int(c)
+        if int(h[:, i, 0].sum()) == 0:
+            return r0 + i + 1
+    return None
+
+
 def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
     """Drive the state machine until no node emits a message.  `ranks`: the
     StateMachineRank objects of this process -- all virtual ranks of one
     topology for a loopback run (exchange None), or independent objects of
     this rank (e.g. pipelined sub-batches) with a DistExchange / SoloExchange
-    `exchange`, whose world they share.  Returns the number of rounds."""
+    `exchange`, whose world they share.  Returns the number of rounds.
+
+    Rounds go out ROUND_BATCH at a time with no host read in between: round r
+    gets the device total of round r - 1's records as `active`, and returns
+    at once when it is 0, so the rounds past quiescence cost an empty launch;
+    one read of the per-round counts per batch finds the quiescent round
+    (round 3 read them back after every round: ~0.3 ms of host gaps per step
+    in the validator-sharded bench objects)."""
+    max_rounds = min(max_rounds, min(sm.max_rounds for sm in ranks))
     if fresh:
         for sm in ranks:
             sm.reset()
     if exchange is not None and exchange.world > 1:
         return _run_rounds_dist(ranks, exchange, max_rounds)
     loop = LoopbackExchange(ranks) if exchange is None and len(ranks) > 1 else None
-    for r in range(max_rounds):
-        for sm in ranks:
-            sm.round(r)
-        counts = [sm.poll() for sm in ranks]
-        for sm, c in zip(ranks, counts):
-            sm.records += c
-        if sum(counts) == 0:
-            return r + 1
-        if loop is not None:
-            loop.gather()
-        else:
+    dev = ranks[0].device
+    act = torch.zeros(max_rounds + 1, dtype=torch.int32, device=dev) if len(ranks) > 1 else None
+    r = 0
+    while r < max_rounds:
+        hi = min(max_rounds, r + ROUND_BATCH)
+        for rr in range(r, hi):
             for sm in ranks:
-                sm.swap_local()
+                if rr == 0:
+                    sm.round(0)
+                else:   # one rank: its own count; several: their device total
+                    sm.round(rr, active=sm.emitted(rr - 1) if act is None else act[rr])
+            if act is not None:
+                act[rr + 1].copy_(torch.stack([sm.emitted(rr) for sm in ranks]).sum())
+            if loop is not None:
+                loop.gather()
+            else:
+                for sm in ranks:
+                    sm.swap_local()
+        h = torch.stack([sm.hist[r:hi] for sm in ranks]).cpu()     # one read per batch
+        done = _check_batch(ranks, h, r)
+        if done is not None:
+            return done
+        r = hi
     raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
 
 
 def _run_rounds_dist(ranks, ex, max_rounds):
     """run_rounds over a process group: ONE all-gather per round carries every
     sub-batch's records and counts plus each one's emitted count and overflow
-    flag (instead of an all-reduce and two all-gathers per sub-batch), and one
-    device-to-host read of the gathered tails decides termination."""
+    flag (instead of an all-reduce and two all-gathers per sub-batch); the
+    next round's `active` is the device sum of the gathered counts, and the
+    gathered tails of a batch of rounds are read back once."""
     dev = ranks[0].device
     parts = [(sm.out.numel(), sm.out_count.numel()) for sm in ranks]
     k = len(ranks)
     body = sum(a + b for a, b in parts)
     send = torch.zeros(body + k + 1, dtype=torch.int32, device=dev)
     recv = torch.empty((ex.world, body + k + 1), dtype=torch.int32, device=dev)
-    for r in range(max_rounds):
-        for sm in ranks:
-            sm.round(r)
-        off = 0
-        for sm, (a, b) in zip(ranks, parts):
-            send[off:off + a].copy_(sm.out.view(-1))
-            send[off + a:off + a + b].copy_(sm.out_count.view(-1))
-            off += a + b
-        tail = torch.stack([sm.emitted for sm in ranks])          # [k][2]
-        send[body:body + k].copy_(tail[:, 0])
-        send[body + k:].copy_(tail[:, 1].amax().view(1))
-        ex.all_gather(recv, send, name="sm_round")
-        t = recv[:, body:].cpu()                                   # [world][k + 1]
-        if int(t[:, k].max()):
-            raise RuntimeError("state machine: a node emitted more than %d messages in a round"
-                               % ranks[0].max_out)
-        for i, sm in enumerate(ranks):
-            sm.records += int(t[ex.rank, i])
-        if int(t[:, :k].sum()) == 0:
-            return r + 1
-        off = 0
-        for sm, (a, b) in zip(ranks, parts):
-            sm.inbox.view(ex.world, a).copy_(recv[:, off:off + a])
-            sm.inbox_count.view(ex.world, b).copy_(recv[:, off + a:off + a + b])
-            off += a + b
+    tails = torch.zeros((max_rounds, ex.world, k + 1), dtype=torch.int32, device=dev)
+    act = torch.zeros(max_rounds + 1, dtype=torch.int32, device=dev)
+    r = 0
+    while r < max_rounds:
+        hi = min(max_rounds, r + ROUND_BATCH)
+        for rr in range(r, hi):
+            for sm in ranks:
+                sm.round(rr, active=None if rr == 0 else act[rr])
+            off = 0
+            for sm, (a, b) in zip(ranks, parts):
+                send[off:off + a].copy_(sm.out.view(-1))
+                send[off + a:off + a + b].copy_(sm.out_count.view(-1))
+                off += a + b
+            hist = torch.stack([sm.hist[rr] for sm in ranks])       # [k][2]
+            send[body:body + k].copy_(hist[:, 0])
+            send[body + k:].copy_(hist[:, 1].amax().view(1))
+            ex.all_gather(recv, send, name="sm_round")
+            tails[rr].copy_(recv[:, body:])
+            act[rr + 1].copy_(recv[:, body:body + k].sum())
+            off = 0
+            for sm, (a, b) in zip(ranks, parts):
+                sm.inbox.view(ex.world, a).copy_(recv[:, off:off + a])
+                sm.inbox_count.view(ex.world, b).copy_(recv[:, off + a:off + a + b])
+                off += a + b
+        t = tails[r:hi].cpu()                                       # [rounds][world][k + 1]
+        # every rank's per-round totals (records of all ranks, overflow of any)
+        h = torch.stack([t[:, :, :k].sum(dim=1).sum(dim=1), t[:, :, k].amax(dim=1)], dim=1)
+        own = t[:, ex.rank, :k].transpose(0, 1)                     # [k][rounds]
+        done = _check_batch(ranks, h.unsqueeze(0), r, own=own)
+        if done is not None:
+            return done
+        r = hi
     raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
 
 

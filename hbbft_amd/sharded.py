@@ -537,7 +537,8 @@ def rank_footprint(n, count, plen, world, rank=0, max_out=4, max_faults=4):
         "own_rows": max(1, len(own)) * 8,
         "echo_cols": max(1, len(echo)) * 8,
         # StateMachineRank (rbc_sim.py) of G * C instances, honest scenario
-        "sm_scenario": G * C * (1 + 3 * n + 2) + G * C * W * 4,
+        # (honest_tensors: role / value_root / value_tamper share one [cnt][n])
+        "sm_scenario": G * C * (1 + n + 2) + G * C * W * 4,
         "sm_state": G * C * R * sm_state,
         "sm_out": G * C * R * max_out * (1 + W) * 4,
         "sm_out_count": G * C * R * 4,

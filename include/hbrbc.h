@@ -509,6 +509,10 @@ typedef struct hbrbc_sm_args {
     uint32_t *fault_count;        /* [count][nodes] (may exceed max_faults) */
     uint32_t *emitted;            /* [2]: [0] += records emitted this round, [1] |= 1 if a
                                      node emitted more than max_out (out_count bit 31) */
+    const uint32_t *active;       /* NULL, or: the round returns at once when *active == 0
+                                     (every sender's previous round emitted nothing: the
+                                     network is quiescent), so a host can enqueue several
+                                     rounds and read the emitted counts back once */
 } hbrbc_sm_args;
 size_t hbrbc_sm_state_bytes(size_t n, size_t roots);
 /* One round for the hosted nodes of every instance (ctx gives n, f, k). */

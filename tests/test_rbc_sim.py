@@ -109,8 +109,9 @@ SINGLE_KINDS = ("honest", "silent", "corrupt_echo", "withhold_echo", "partial_va
 
 def make_single_root_instances(n, rng, seed_tag=0):
     """Scenario instances with ONE codeword each (Scenario.roots == 1), the
-    form the validator-sharded runs use (sim.hip Sm<true>: one-byte Echo /
-    Ready entries, counters and flags in registers): every adversary that
+    form the validator-sharded runs use (sim.hip Sm<true>: Echo / Ready
+    entries as four 32-sender bitmasks, counters and flags in registers):
+    every adversary that
     needs no second value -- silent faulty nodes (the ProposeAdversary's drop
     without its injected broadcasts), corrupted or withheld Echoes, a faulty
     proposer that sends nothing or tampered proofs to some validators, and a
@@ -350,24 +351,30 @@ def test_state_machine_counters_at_size():
 class _FakeSm:
     """A StateMachineRank stand-in with the buffers _run_rounds_dist moves:
     round r of rank g, sub-batch b writes records tagged (g, b, r) and emits
-    until round 2 (rank 1's sub-batch 1 until round 3)."""
+    until round 2 (rank 1's sub-batch 1 until round 3); like the kernel, a
+    round whose `active` total is 0 returns at once."""
 
-    def __init__(self, rank, world, b, count=3, R=2, E=2, rec=2):
+    def __init__(self, rank, world, b, count=3, R=2, E=2, rec=2, max_rounds=16):
         self.rank, self.b, self.max_out = rank, b, E
         self.device = torch.device("cpu")
+        self.max_rounds = max_rounds
         self.out = torch.zeros((count, R, E, rec), dtype=torch.int32)
         self.out_count = torch.zeros((count, R), dtype=torch.int32)
         self.inbox = torch.zeros((world, count, R, E, rec), dtype=torch.int32)
         self.inbox_count = torch.zeros((world, count, R), dtype=torch.int32)
-        self.emitted = torch.zeros(2, dtype=torch.int32)
+        self.hist = torch.zeros((max_rounds, 2), dtype=torch.int32)
         self.records = 0
         self.last = 2 if (rank, b) != (1, 1) else 3
+        self.ran = []
 
-    def round(self, r):
-        active = r <= self.last
+    def round(self, r, active=None):
+        if active is not None and int(active) == 0:
+            return
+        self.ran.append(r)
+        emits = r <= self.last
         self.out.fill_(self.rank * 10000 + self.b * 1000 + r)
-        self.out_count.fill_(1 if active else 0)
-        self.emitted[0] = self.out_count.numel() if active else 0
+        self.out_count.fill_(1 if emits else 0)
+        self.hist[r, 0] = self.out_count.numel() if emits else 0
 
 
 def _gloo_dist_rounds_worker(rank, world, port, q):
@@ -382,10 +389,12 @@ def _gloo_dist_rounds_worker(rank, world, port, q):
         rounds = _run_rounds_dist(sms, DistExchange(), 16)
         good = rounds == 5   # the last emission (round 3) is delivered, round 4 is silent
         for sm in sms:
-            # the inbox holds every rank's records of round 3 for this sub-batch
+            # rounds 0..4 ran; round 5 (enqueued in the same batch) saw active 0
+            good &= sm.ran == [0, 1, 2, 3, 4]
+            # the inbox holds every rank's records of round 4, the silent one
             for g in range(world):
-                good &= bool((sm.inbox[g] == g * 10000 + sm.b * 1000 + 3).all())
-                good &= bool((sm.inbox_count[g] == (1 if (g, sm.b) == (1, 1) else 0)).all())
+                good &= bool((sm.inbox[g] == g * 10000 + sm.b * 1000 + 4).all())
+                good &= bool((sm.inbox_count[g] == 0).all())
             good &= sm.records == sm.out_count.numel() * (sm.last + 1)
         q.put((rank, "ok" if good else "mismatch rounds=%d" % rounds))
     except Exception as e:  # pragma: no cover

@@ -320,3 +320,55 @@ def test_sharded_two_ranks_gloo_on_one_gpu():
     for p in procs:
         p.join(60)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+# ----------------------------------------------------------- HBM footprint --
+BENCH_OBJECTS = [("cfg3", 64, 256 << 10, 4096), ("cfg4", 128, 256 << 10, 2048)]
+
+
+@pytest.mark.parametrize("cfg,n,plen,count", BENCH_OBJECTS)
+def test_rank_footprint_fits_hbm(cfg, n, plen, count):
+    """Every rank of the bench's validator-sharded objects fits one MI355X
+    (288 GB) at 1, 2, 4 and 8 GPUs: echo slab [G][G*C][R][stride], proposer
+    slab, decode trees, state machine inboxes [G][G*C][R][E][1+W] and the
+    library's reconstruct workspace (upper bound)."""
+    from hbbft_amd.sharded import HBM_PER_GPU, rank_footprint
+    prev = 0
+    for world in (1, 2, 4, 8):
+        for rank in (0, world - 1):
+            fp = rank_footprint(n, count, plen, world, rank)
+            assert fp["total_bytes"] < HBM_PER_GPU, (cfg, world, rank, fp["total_bytes"])
+            assert all(v > 0 for v in fp["buffers"].values())
+        # the all-gathered echo slab grows with the world (every rank decodes all)
+        assert fp["torch_bytes"] > prev
+        prev = fp["torch_bytes"]
+    fp8 = rank_footprint(n, count, plen, 8, 0)
+    # the G=8 echo slab dominates: G * G*C * R * stride bytes
+    R = -(-n // 8)
+    assert fp8["buffers"]["echo_sh"] == 8 * 8 * count * R * ((-(-(plen + 4) // (n - 2 * ((n - 1) // 3))) + 15) // 16 * 16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,world,count,plen", [(64, 1, 64, 50000), (64, 8, 16, 50000),
+                                                (128, 4, 16, 30000)])
+def test_rank_footprint_matches_allocation(n, world, count, plen):
+    """rank_footprint's torch buffers equal what ShardedBroadcast allocates
+    (torch.cuda.memory_allocated delta; ranks of a larger world can be built
+    on one GPU -- no collective runs)."""
+    import torch
+
+    from hbbft_amd.sharded import ShardedBroadcast, rank_footprint
+
+    def requested():
+        # bytes the tensors asked for (before the caching allocator rounds
+        # them up or hands out a whole unsplit segment tail)
+        return torch.cuda.memory_stats(0).get("requested_bytes.all.current")
+
+    torch.cuda.synchronize()
+    before = requested()
+    sb = ShardedBroadcast(n, count, plen, 0, world, device=0, specialise=False)
+    torch.cuda.synchronize()
+    got = requested() - before
+    want = rank_footprint(n, count, plen, world, 0)["torch_bytes"]
+    assert got == want, (got, want, got - want)
+    del sb

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=$ROOT/gpurun_out/pmc_${TAG:-stall}
 mkdir -p $OUT
 REGEX=${REGEX:-hbrbc_enc|hbrbc_dec|gf_bitslice|leaf_hash|validate_kernel}
-ARGS="--config ${CONFIG:-cfg3} --steps 1 --warmup 1 --no-cpu --mode instances --no-verify --no-leaf-reuse"
+ARGS="--config ${CONFIG:-cfg3} --steps 1 --warmup 1 --no-cpu --mode ${MODE:-instances} --no-verify --no-leaf-reuse --f4-checks 0"
 i=0
 # SETS="group1|group2|..." replaces the default counter groups
 if [ -n "$SETS" ]; then IFS='|' read -r -a GROUPS_ <<< "$SETS"; else GROUPS_=(); fi
