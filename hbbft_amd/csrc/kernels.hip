@@ -316,6 +316,49 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
             bs_transpose(x);
             // RT coefficient bytes of this input for this pass (16-byte padded)
             const uint32_t c4[4] = {cw.x, cw.y, cw.z, cw.w};
+            if constexpr (MODE == 3) {
+                // Bit pairs (b, b + 1): when both bits of a coefficient are set,
+                // one v_bitop3 per plane folds 2^b x and 2^(b+1) x into the
+                // accumulator at once (24 instead of 32 VALU per coefficient on
+                // average).  Both multiples are live together: the doubling
+                // to 2^(b+1) x rewrites only three planes, whose old values are
+                // kept in o[] (3 VGPRs).
+#pragma unroll
+                for (int b = 0; b < 8; b += 2) {
+                    const uint32_t h = x[(7 - b) & 7];
+                    const uint32_t o[3] = {x[(1 - b) & 7], x[(2 - b) & 7], x[(3 - b) & 7]};
+                    x[(1 - b) & 7] ^= h;
+                    x[(2 - b) & 7] ^= h;
+                    x[(3 - b) & 7] ^= h;
+                    // logical plane q of 2^b x (before this doubling)
+                    auto lo_plane = [&](int q) {
+                        const int i = (q - b) & 7;
+                        return i == ((1 - b) & 7) ? o[0] : i == ((2 - b) & 7) ? o[1]
+                                                         : i == ((3 - b) & 7) ? o[2] : x[i];
+                    };
+#pragma unroll
+                    for (int t = 0; t < RT; ++t) {
+                        const uint32_t two = (c4[t >> 2] >> (8 * (t & 3) + b)) & 3u;
+                        if (two == 3u) {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) acc[t][q] ^= lo_plane(q) ^ x[(q - b - 1) & 7];
+                        } else if (two == 1u) {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) acc[t][q] ^= lo_plane(q);
+                        } else if (two == 2u) {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) acc[t][q] ^= x[(q - b - 1) & 7];
+                        }
+                    }
+                    if (b < 6) {   // to 2^(b+2) x for the next pair
+                        const uint32_t h2 = x[(6 - b) & 7];
+                        x[(0 - b) & 7] ^= h2;
+                        x[(1 - b) & 7] ^= h2;
+                        x[(2 - b) & 7] ^= h2;
+                    }
+                }
+                return;
+            }
             // At step b the planes of 2^b * x sit rotated: logical plane q is
             // x[(q - b) & 7], so doubling moves no registers, only XORs h into
             // logical planes 2, 3, 4 (x^8 = x^4 + x^3 + x^2 + 1).
@@ -1252,7 +1295,9 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
                        piece, a.payload, a.payload_stride, a.payload_S, a.payload_k, a.rstatus)
 #define HB_BS_CASE(RT)                                                                           \
     case RT:                                                                                     \
-        if (a.mode == 2)                                                                         \
+        if (a.mode == 3)                                                                         \
+            HB_BS_LAUNCH(RT, 3);                                                                 \
+        else if (a.mode == 2)                                                                    \
             HB_BS_LAUNCH(RT, 2);                                                                 \
         else if (a.mode == 1)                                                                    \
             HB_BS_LAUNCH(RT, 1);                                                                 \

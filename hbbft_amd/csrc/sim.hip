@@ -114,67 +114,112 @@ struct Sm {
     const uint8_t *pok;       // this instance's proof_ok [C][2][n]
     const uint8_t *dok;       // this instance's decode_ok [C]
 
-    __device__ uint32_t ECHO(int s) const {
+    // ONE: the mask word of the 32 senders the inbox loop is at lives in
+    // registers (cache, word cw; the loop walks senders in order, so it moves
+    // once per 32 senders): the handlers' read-modify-writes of a sender's
+    // entry cost no LDS round trip.  Other words (a node's own entry, the
+    // full-Echo masks of a CanDecode) go to LDS.
+    uint4 cache = {0u, 0u, 0u, 0u};
+    int cw = -1;
+    __device__ __forceinline__ uint4 em_get(int w) const {
+        // a select of values, not of addresses (a pointer select between the
+        // register copy and LDS would put the whole Sm object on the stack)
+        // -- LLVM folds "if (c) v = *p else v = *q" into a load through a
+        // selected pointer; the empty asm keeps the register arm a register)
+        uint4 v;
+        if (w == cw) {
+            v = cache;
+            __asm__ volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+        } else {
+            v = em[(size_t)w * sd];
+        }
+        return v;
+    }
+    __device__ __forceinline__ void em_put(int w, const uint4 &v) {
+        if (w == cw) {
+            uint4 t = v;
+            __asm__ volatile("" : "+v"(t.x), "+v"(t.y), "+v"(t.z), "+v"(t.w));
+            cache = t;
+        } else {
+            em[(size_t)w * sd] = v;
+        }
+    }
+    __device__ __forceinline__ void em_focus(int w) {   // w uniform across the wave
         if constexpr (ONE) {
-            const uint4 v = em[(size_t)(s >> 5) * sd];
+            if (w == cw) return;
+            if (cw >= 0) em[(size_t)cw * sd] = cache;
+            cache = em[(size_t)w * sd];
+            cw = w;
+        }
+    }
+    __device__ __forceinline__ void em_flush() {
+        if constexpr (ONE) {
+            if (cw >= 0) em[(size_t)cw * sd] = cache;
+            cw = -1;
+        }
+    }
+    __device__ __forceinline__ uint32_t ECHO(int s) const {
+        if constexpr (ONE) {
+            const uint4 v = em_get(s >> 5);
             const uint32_t b = 1u << (s & 31);
             return (v.y & b) ? (0x20u | ((v.z & b) ? 8u : 0u)) : ((v.x & b) ? 0x10u : 0u);
         } else {
             return er16[(size_t)s * sd] & 0xFFu;
         }
     }
-    __device__ void set_echo(int s, uint32_t e) {
+    __device__ __forceinline__ void set_echo(int s, uint32_t e) {
         if constexpr (ONE) {
-            uint4 &v = em[(size_t)(s >> 5) * sd];
             const uint32_t b = 1u << (s & 31);
-            uint4 t = v;
+            uint4 t = em_get(s >> 5);
             t.x = (e & 0x10u) ? (t.x | b) : (t.x & ~b);
             t.y = (e & 0x20u) ? (t.y | b) : (t.y & ~b);
             t.z = (e & 0x28u) == 0x28u ? (t.z | b) : (t.z & ~b);
-            v = t;
+            em_put(s >> 5, t);
         } else {
             uint16_t &w = er16[(size_t)s * sd];
             w = (uint16_t)((w & 0xFF00u) | e);
         }
     }
-    __device__ uint32_t READY(int s) const {
-        if constexpr (ONE) return (em[(size_t)(s >> 5) * sd].w >> (s & 31)) & 1u;
+    __device__ __forceinline__ uint32_t READY(int s) const {
+        if constexpr (ONE) return (em_get(s >> 5).w >> (s & 31)) & 1u;
         else return er16[(size_t)s * sd] >> 8;
     }
-    __device__ void set_ready(int s, uint32_t r) {
+    __device__ __forceinline__ void set_ready(int s, uint32_t r) {
         if constexpr (ONE) {
-            uint32_t &m = reinterpret_cast<uint32_t *>(&em[(size_t)(s >> 5) * sd])[3];
             const uint32_t b = 1u << (s & 31);
-            m = r ? (m | b) : (m & ~b);
+            uint4 t = em_get(s >> 5);
+            t.w = r ? (t.w | b) : (t.w & ~b);
+            em_put(s >> 5, t);
         } else {
             uint16_t &w = er16[(size_t)s * sd];
             w = (uint16_t)((w & 0xFFu) | (r << 8));
         }
     }
-    __device__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
-    __device__ uint32_t &FULL(int w) {
-        if constexpr (ONE) return reinterpret_cast<uint32_t *>(&em[(size_t)w * sd])[1];
+    __device__ __forceinline__ uint32_t &CAND(uint32_t c, int w) { return cand[((size_t)c * W + w) * sd]; }
+    __device__ __forceinline__ uint32_t &FULL(int w) { return full[(size_t)w * sd]; }   // (several roots)
+    __device__ __forceinline__ uint32_t full_word(int w) const {
+        if constexpr (ONE) return em_get(w).y;
         else return full[(size_t)w * sd];
     }
     uint16_t r_ce = 0, r_cf = 0, r_cr = 0;
     uint32_t r_flags = 0;
-    __device__ uint16_t &CE(uint32_t c) {
+    __device__ __forceinline__ uint16_t &CE(uint32_t c) {
         if constexpr (ONE) return r_ce;
         else return cnt[(size_t)c * sd];
     }
-    __device__ uint16_t &CF(uint32_t c) {
+    __device__ __forceinline__ uint16_t &CF(uint32_t c) {
         if constexpr (ONE) return r_cf;
         else return cnt[((size_t)C + c) * sd];
     }
-    __device__ uint16_t &CR(uint32_t c) {
+    __device__ __forceinline__ uint16_t &CR(uint32_t c) {
         if constexpr (ONE) return r_cr;
         else return cnt[((size_t)2 * C + c) * sd];
     }
-    __device__ uint32_t &FLAGS() {
+    __device__ __forceinline__ uint32_t &FLAGS() {
         if constexpr (ONE) return r_flags;
         else return *flags;
     }
-    __device__ void cache_in() {
+    __device__ __forceinline__ void cache_in() {
         if constexpr (ONE) {
             r_ce = cnt[0];
             r_cf = cnt[sd];
@@ -182,7 +227,7 @@ struct Sm {
             r_flags = *flags;
         }
     }
-    __device__ void cache_out() {
+    __device__ __forceinline__ void cache_out() {
         if constexpr (ONE) {
             cnt[0] = r_ce;
             cnt[sd] = r_cf;
@@ -196,20 +241,20 @@ struct Sm {
     uint16_t *faults;
     uint32_t nfault;
 
-    __device__ bool bit(const uint32_t *m, int i) const { return (m[i >> 5] >> (i & 31)) & 1u; }
+    __device__ __forceinline__ bool bit(const uint32_t *m, int i) const { return (m[i >> 5] >> (i & 31)) & 1u; }
 
-    __device__ void fault(int node, int kind) {
+    __device__ __forceinline__ void fault(int node, int kind) {
         if (nfault < a.max_faults) faults[nfault] = (uint16_t)((node << 8) | kind);
         ++nfault;
     }
 
     // right_nodes (broadcast.rs:476-485): the f nodes before us on the circle
-    __device__ bool is_right_of(int j, int i) const {
+    __device__ __forceinline__ bool is_right_of(int j, int i) const {
         const int d = (i - j + n) % n;   // j = i - d
         return d >= 1 && d <= f;
     }
 
-    __device__ uint32_t *emit_rec(uint32_t kind, uint32_t c, uint32_t j, uint32_t t) {
+    __device__ __forceinline__ uint32_t *emit_rec(uint32_t kind, uint32_t c, uint32_t j, uint32_t t) {
         if (nout >= a.max_out) {
             overflow = true;
             return nullptr;
@@ -224,29 +269,29 @@ struct Sm {
     // lanes of a wave reach a send at different senders, so a per-node loop
     // would run once per distinct trigger point).  lin(w, a, b): bits [a, b)
     // of word w.
-    __device__ static uint32_t lin(int w, int a, int b) {
+    __device__ __forceinline__ static uint32_t lin(int w, int a, int b) {
         const int lo = a > 32 * w ? a : 32 * w, hi = b < 32 * w + 32 ? b : 32 * w + 32;
         if (hi <= lo) return 0u;
         const int len = hi - lo;
         return (len >= 32 ? 0xFFFFFFFFu : ((1u << len) - 1u)) << (lo - 32 * w);
     }
-    __device__ uint32_t all_but_me(int w) const {
+    __device__ __forceinline__ uint32_t all_but_me(int w) const {
         return lin(w, 0, n) & ~((me >> 5) == w ? 1u << (me & 31) : 0u);
     }
     // right_nodes(me) (broadcast.rs:476-485): [me - f, me) on the circle
-    __device__ uint32_t right_mask(int w) const {
+    __device__ __forceinline__ uint32_t right_mask(int w) const {
         const int a0 = me - f;
         return a0 >= 0 ? lin(w, a0, me) : (lin(w, 0, me) | lin(w, a0 + n, n));
     }
     template <class M>
-    __device__ void targets_w(uint32_t *r, M mask) {
+    __device__ __forceinline__ void targets_w(uint32_t *r, M mask) {
         for (int w = 0; w < W; ++w) r[1 + w] = mask(w);
     }
 
     // the recipient mask of record r: bit i set iff pred(i), each word built
     // in a register and stored once (the caller fills every emitted record)
     template <class P>
-    __device__ void targets(uint32_t *r, P pred) {
+    __device__ __forceinline__ void targets(uint32_t *r, P pred) {
         for (int w = 0; w < W; ++w) {
             uint32_t mk = 0;
             const int hi = n - 32 * w < 32 ? n - 32 * w : 32;
@@ -257,20 +302,20 @@ struct Sm {
     }
 
     // emission as the node's own step (subject to its role)
-    __device__ uint32_t *emit(uint32_t kind, uint32_t c, uint32_t j = 0, uint32_t t = 0) {
+    __device__ __forceinline__ uint32_t *emit(uint32_t kind, uint32_t c, uint32_t j = 0, uint32_t t = 0) {
         if (drop) return nullptr;
         if (kind == K_ECHO && role == R_WITHHOLD_ECHO) return nullptr;
         if (kind == K_ECHO && role == R_CORRUPT_ECHO) t = 1;
         return emit_rec(kind, c, j, t);
     }
 
-    __device__ bool validate_proof(uint32_t c, uint32_t j, uint32_t t, int sender) const {
+    __device__ __forceinline__ bool validate_proof(uint32_t c, uint32_t j, uint32_t t, int sender) const {
         if ((int)j != sender || c >= (uint32_t)C || j >= (uint32_t)n) return false;
         return pok[(c * 2 + (t & 1)) * n + j] != 0;
     }
 
     // -- handlers (broadcast.rs) --------------------------------------------
-    __device__ void compute_output(uint32_t c) {   // 526-558
+    __device__ __forceinline__ void compute_output(uint32_t c) {   // 526-558
         if ((FLAGS() & FL_DECIDED) || CR(c) <= 2 * f || CF(c) < k) return;
         if (dok[c]) {
             FLAGS() |= FL_DECIDED;
@@ -280,7 +325,7 @@ struct Sm {
         }
     }
 
-    __device__ void send_echo_remaining(uint32_t c) {   // 428-453
+    __device__ __forceinline__ void send_echo_remaining(uint32_t c) {   // 428-453
         FLAGS() |= FL_ECHO_SENT;
         const uint32_t e = ECHO(me);
         if (!is_full(e) || root_of(e) != c) return;
@@ -289,72 +334,85 @@ struct Sm {
         targets_w(r, [&](int w) { return right_mask(w) & ~CAND(c, w); });
     }
 
-    __device__ void handle_ready_core(int s, uint32_t c, bool may_send);
+    __device__ __forceinline__ void handle_ready_core(int s, uint32_t c, bool may_send);
 
-    __device__ void send_ready(uint32_t c) {   // 513-522
+    __device__ __forceinline__ void send_ready(uint32_t c) {   // 513-522
         FLAGS() |= FL_READY_SENT;
         uint32_t *r = emit(K_READY, c);
         if (r) targets_w(r, [&](int w) { return all_but_me(w); });
         handle_ready_core(me, c, false);
     }
 
-    __device__ void handle_can_decode(int s, uint32_t c) {   // 358-375
+    __device__ __forceinline__ void handle_can_decode(int s, uint32_t c) {   // 358-375
         CAND(c, s >> 5) |= 1u << (s & 31);
     }
 
-    __device__ void send_can_decode(uint32_t c) {   // 488-510
+    __device__ __forceinline__ void send_can_decode(uint32_t c) {   // 488-510
         FLAGS() |= 1u << (FL_CAN_DECODE_SHIFT + c);
         uint32_t *r = emit(K_CAN_DECODE, c);
-        if (r) targets_w(r, [&](int w) { return all_but_me(w) & ~FULL(w); });
+        if (r) targets_w(r, [&](int w) { return all_but_me(w) & ~full_word(w); });
         handle_can_decode(me, c);
     }
 
-    __device__ void handle_echo(int s, uint32_t c, uint32_t j, uint32_t t) {   // 266-320
+    // handle_echo (266-320, full = true) and handle_echo_hash (322-355, full =
+    // false) in one body: the checks and faults differ per kind, the counter
+    // updates, the entry and the thresholds are shared code, so a wave whose
+    // lanes take different kinds for the same sender (Echo for the left
+    // nodes, EchoHash for the right ones) runs the common part once.
+    __device__ __forceinline__ void handle_echo_any(int s, uint32_t c, uint32_t j, uint32_t t,
+                                                    bool full) {
         const uint32_t e = ECHO(s);
-        if (is_full(e)) {   // the stored proof is (root_of(e), s, tamper_of(e))
-            if (e != enc_full(c, t) || (int)j != s) fault(s, F_MULTIPLE_ECHOS);
-            return;
+        int fk = -1;
+        bool stop = false;
+        if (full) {
+            if (is_full(e)) {   // the stored proof is (root_of(e), s, tamper_of(e))
+                if (e != enc_full(c, t) || (int)j != s) fk = F_MULTIPLE_ECHOS;
+                stop = true;
+            } else if (is_hash(e) && root_of(e) != c) {
+                fk = F_MULTIPLE_ECHOS;
+                stop = true;
+            } else if (!validate_proof(c, j, t, s)) {
+                fk = F_INVALID_PROOF;
+                stop = true;
+            }
+        } else if (e) {
+            if (root_of(e) != c) fk = F_MULTIPLE_ECHO_HASHES;
+            stop = true;
         }
-        if (is_hash(e) && root_of(e) != c) {
-            fault(s, F_MULTIPLE_ECHOS);
-            return;
+        if (fk >= 0) fault(s, fk);
+        if (stop) return;
+        if (!e) ++CE(c);   // (full: a Hash of the same root was counted already)
+        if (full) {
+            ++CF(c);
+            if constexpr (!ONE) FULL(s >> 5) |= 1u << (s & 31);
         }
-        if (!validate_proof(c, j, t, s)) {
-            fault(s, F_INVALID_PROOF);
-            return;
-        }
-        if (!e) ++CE(c);   // a Hash of the same root was counted already
-        ++CF(c);
-        set_echo(s, enc_full(c, t));   // (ONE: sets the full-Echo bit too)
-        if constexpr (!ONE) FULL(s >> 5) |= 1u << (s & 31);
-        if (!(FLAGS() & (1u << (FL_CAN_DECODE_SHIFT + c))) && CF(c) >= k) send_can_decode(c);
-        if (!(FLAGS() & FL_READY_SENT) && CE(c) >= n - f) send_ready(c);
-        if (FLAGS() & FL_READY_SENT) compute_output(c);
-    }
-
-    __device__ void handle_echo_hash(int s, uint32_t c) {   // 322-355
-        const uint32_t e = ECHO(s);
-        if (e) {
-            if (root_of(e) != c) fault(s, F_MULTIPLE_ECHO_HASHES);
-            return;
-        }
-        set_echo(s, enc_hash(c));
-        ++CE(c);
-        if ((FLAGS() & FL_READY_SENT) || CE(c) < n - f) {
+        set_echo(s, full ? enc_full(c, t) : enc_hash(c));   // (ONE: the full bit too)
+        if (full && !(FLAGS() & (1u << (FL_CAN_DECODE_SHIFT + c))) && CF(c) >= k)
+            send_can_decode(c);
+        // Echo: send Ready at N - f, then compute_output once Ready is sent;
+        // EchoHash: send Ready at N - f, else compute_output
+        if (!(FLAGS() & FL_READY_SENT) && CE(c) >= n - f) {
+            send_ready(c);
+            if (full) compute_output(c);
+        } else if (!full || (FLAGS() & FL_READY_SENT)) {
             compute_output(c);
-            return;
         }
-        send_ready(c);
+    }
+    __device__ __forceinline__ void handle_echo(int s, uint32_t c, uint32_t j, uint32_t t) {
+        handle_echo_any(s, c, j, t, true);
+    }
+    __device__ __forceinline__ void handle_echo_hash(int s, uint32_t c) {
+        handle_echo_any(s, c, 0, 0, false);
     }
 
-    __device__ void send_echo_hash(uint32_t c) {   // 456-468
+    __device__ __forceinline__ void send_echo_hash(uint32_t c) {   // 456-468
         FLAGS() |= FL_ECHO_HASH_SENT;
         uint32_t *r = emit(K_ECHO_HASH, c);
         if (r) targets_w(r, [&](int w) { return right_mask(w); });
         handle_echo_hash(me, c);
     }
 
-    __device__ void send_echo_left(uint32_t c, uint32_t j, uint32_t t) {   // 413-425
+    __device__ __forceinline__ void send_echo_left(uint32_t c, uint32_t j, uint32_t t) {   // 413-425
         uint32_t *r = emit(K_ECHO, c, j, t);
         if (r) targets_w(r, [&](int w) { return all_but_me(w) & ~right_mask(w); });
         handle_echo(me, c, j, t);
@@ -363,7 +421,7 @@ struct Sm {
     // rotate out[a0, a1) behind out[a1, nout) (and the same for faults):
     // echo_steps.join(echo_hash_steps) lists the Echo step first although the
     // EchoHash step ran first (broadcast.rs:258-262)
-    __device__ void rotate_tail(uint32_t m0, uint32_t m1, uint32_t f0, uint32_t f1) {
+    __device__ __forceinline__ void rotate_tail(uint32_t m0, uint32_t m1, uint32_t f0, uint32_t f1) {
         // messages: at most max_out records, rotated one record at a time
         const uint32_t nb = m1 - m0, na = nout - m1;
         for (uint32_t s = 0; s < nb; ++s) {   // move record m0 to the end, nb times
@@ -385,7 +443,7 @@ struct Sm {
         }
     }
 
-    __device__ void handle_value(int s, uint32_t c, uint32_t j, uint32_t t) {   // 228-263
+    __device__ __forceinline__ void handle_value(int s, uint32_t c, uint32_t j, uint32_t t) {   // 228-263
         if (s != proposer) {
             fault(s, F_VALUE_FROM_NON_PROPOSER);
             return;
@@ -413,7 +471,7 @@ struct Sm {
     // order) its fresh Broadcast's messages -- Value(proof j) to every j != F,
     // Echo(proof F) to AllExcept(right(F)), EchoHash to right(F) -- all sent
     // by the dispatching node; a receiver handles the ones addressed to it
-    __device__ void handle_fake(int s, uint32_t c) {
+    __device__ __forceinline__ void handle_fake(int s, uint32_t c) {
         const uint32_t *list = a.fake_list + inst * W;
         for (int F = 0; F < n; ++F) {
             if (!bit(list, F)) continue;
@@ -423,7 +481,7 @@ struct Sm {
         }
     }
 
-    __device__ void deliver(int s, const uint32_t *r) {
+    __device__ __forceinline__ void deliver(int s, const uint32_t *r) {
         const uint32_t kind = r[0] & 0xFFu, c0 = (r[0] >> 8) & 0xFFu;
         const uint32_t j = (r[0] >> 16) & 0xFFu, t = (r[0] >> 24) & 0xFFu;
         switch (kind) {
@@ -438,10 +496,12 @@ struct Sm {
                 handle_value(s, c, (uint32_t)me, tt);
                 break;
             }
-            case K_ECHO: handle_echo(s, c0, j, t); break;
+            case K_ECHO:   // one inlined body for both kinds (lanes of a merged
+            case K_ECHO_HASH:   // Echo / EchoHash step take different kinds)
+                handle_echo_any(s, c0, j, t, kind == K_ECHO);
+                break;
             case K_READY: handle_ready_core(s, c0, true); break;
             case K_CAN_DECODE: handle_can_decode(s, c0); break;
-            case K_ECHO_HASH: handle_echo_hash(s, c0); break;
             case K_FAKE: handle_fake(s, c0); break;
             default: break;
         }
@@ -449,7 +509,7 @@ struct Sm {
 };
 
 template <bool ONE>
-__device__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {   // 378-410
+__device__ __forceinline__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {   // 378-410
     const uint32_t old = READY(s);
     if (old) {
         if (old - 1 != c) fault(s, F_MULTIPLE_READYS);
@@ -470,7 +530,7 @@ __device__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {  
 // one root); counters u16[3][C]; flags u32).
 struct SmLayout {
     size_t er, cand, full, cnt, flags;
-    __device__ SmLayout(int n, int C, int W, size_t sd) {
+    __device__ __forceinline__ SmLayout(int n, int C, int W, size_t sd) {
         er = 0;
         cand = (sm_er_bytes((size_t)n, (size_t)C) * sd + 3) & ~(size_t)3;
         full = cand + 4 * (size_t)C * W * sd;
@@ -483,7 +543,7 @@ struct SmLayout {
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
 // `inc(s)` sender s's record count, `recs(s)` its records.
 template <bool ONE, class InCount, class Recs>
-__device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
+__device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
                         InCount inc, Recs recs) {
     const int me = (int)a.node_lo + local;
@@ -533,12 +593,32 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
         m.drop = m.role == R_SILENT;
         const bool faker = a.fake_from[inst] == (uint8_t)me;
         for (int s = 0; s < n; ++s) {
+            m.em_focus(s >> 5);
             if (s == me) continue;   // targets never include the sender
             const uint32_t cnt = inc(s);
             const uint32_t *rs = recs(s);
             for (uint32_t e = 0; e < cnt; ++e) {
                 const uint32_t *r = rs + (size_t)e * (1 + W);
-                if (!m.bit(r + 1, me)) continue;
+                const uint32_t k0 = r[0] & 0xFFu;
+                bool hit = m.bit(r + 1, me);
+                // An Echo and an EchoHash of the same sender in a row whose
+                // targets do not overlap at this node (handle_value emits
+                // Echo to all but the right nodes, EchoHash to the right
+                // ones): this node handles at most one of them, so both are
+                // taken in one step through the merged handler.
+                if ((k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
+                    const uint32_t *r2 = r + (1 + W);
+                    const uint32_t k1 = r2[0] & 0xFFu;
+                    const bool hit2 = m.bit(r2 + 1, me);
+                    if ((k1 == K_ECHO || k1 == K_ECHO_HASH) && k1 != k0 && !(hit && hit2)) {
+                        ++e;
+                        if (hit2) {
+                            r = r2;
+                            hit = true;
+                        }
+                    }
+                }
+                if (!hit) continue;
                 m.deliver(s, r);
                 if (faker && !(m.FLAGS() & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
@@ -549,6 +629,7 @@ __device__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, s
             }
         }
     }
+    m.em_flush();
     m.cache_out();
     a.out_count[g] = m.nout | (m.overflow ? 0x80000000u : 0u);
     a.fault_count[g] = m.nfault;
