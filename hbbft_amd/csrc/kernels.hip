@@ -1284,7 +1284,16 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     const size_t blocks = (size_t)wpr * a.count;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const int max_rows = a.nout ? a.max_rows : a.nout_uniform;
-    const int nw = std::max(1, std::min(4, (max_rows + a.rt - 1) / a.rt));  // waves per block
+    // waves per block: the fewest that keep the longest wave at the minimum
+    // number of passes (a wave beyond an instance's passes exits at once, but
+    // its slot in the block idles a SIMD: cfg3, 42 rows at most in 7-row
+    // passes, 3 waves instead of 4 -> reconstruct 3.29 -> 3.11-3.17 ms)
+    const int npass_max = std::max(1, (max_rows + a.rt - 1) / a.rt);
+    const int path = (npass_max + 3) / 4;
+    int nw = std::max(1, std::min(4, (npass_max + path - 1) / path));
+    // HBRBC_GF_WAVES=1..4: waves per block (A/B; a wave beyond the passes of
+    // an instance exits at once)
+    if (const char *we = getenv("HBRBC_GF_WAVES")) nw = std::max(1, std::min(4, atoi(we)));
     const char *pe = getenv("HBRBC_GF_SPLIT");   // 0: 32 consecutive bytes per lane (A/B)
     const uint32_t piece = (pe && !strcmp(pe, "0")) ? 16u : 1024u;
 #define HB_BS_LAUNCH(RT, MODE)                                                                   \

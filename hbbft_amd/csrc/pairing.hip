@@ -165,43 +165,48 @@ DEV void fp_from29(Fp &r, const uint32_t (&o)[14], bool neg) {
     fp_reduce_once(r, t);
 }
 
+// HB_FP_CHAINS: independent 64-bit accumulators per column (the products of a
+// column are split round-robin over them; each v_mad_u64_u32 depends on the
+// previous one of its chain).  A/B: 2 (round 3) or 4.
+#ifndef HB_FP_CHAINS
+#define HB_FP_CHAINS 2
+#endif
 DEV void fp_mul(Fp &r, const Fp &a, const Fp &b) {
+    constexpr int NC = HB_FP_CHAINS;
     uint32_t x[14], y[14], m[14], o[14];
     fp_to29(x, a.l);
     fp_to29(y, b.l);
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 14; ++k) {
-        uint64_t e = acc, f = 0;
+        uint64_t e[NC];
 #pragma unroll
-        for (int i = 0; i <= k; ++i) {
-            if (i & 1) f += (uint64_t)x[i] * y[k - i];
-            else e += (uint64_t)x[i] * y[k - i];
-        }
+        for (int c = 0; c < NC; ++c) e[c] = c ? 0 : acc;
+        int q = 0;
 #pragma unroll
-        for (int i = 0; i < k; ++i) {
-            if (i & 1) f += (uint64_t)m[i] * kP29[k - i];
-            else e += (uint64_t)m[i] * kP29[k - i];
-        }
-        acc = e + f;
+        for (int i = 0; i <= k; ++i, ++q) e[q % NC] += (uint64_t)x[i] * y[k - i];
+#pragma unroll
+        for (int i = 0; i < k; ++i, ++q) e[q % NC] += (uint64_t)m[i] * kP29[k - i];
+        acc = e[0];
+#pragma unroll
+        for (int c = 1; c < NC; ++c) acc += e[c];
         m[k] = ((uint32_t)acc * kPinv29) & kM29;
         acc += (uint64_t)m[k] * kP29[0];   // low 29 bits become 0
         acc >>= 29;
     }
 #pragma unroll
     for (int k = 14; k < 27; ++k) {
-        uint64_t e = acc, f = 0;
+        uint64_t e[NC];
 #pragma unroll
-        for (int i = k - 13; i < 14; ++i) {
-            if (i & 1) f += (uint64_t)x[i] * y[k - i];
-            else e += (uint64_t)x[i] * y[k - i];
-        }
+        for (int c = 0; c < NC; ++c) e[c] = c ? 0 : acc;
+        int q = 0;
 #pragma unroll
-        for (int i = k - 13; i < 14; ++i) {
-            if (i & 1) f += (uint64_t)m[i] * kP29[k - i];
-            else e += (uint64_t)m[i] * kP29[k - i];
-        }
-        acc = e + f;
+        for (int i = k - 13; i < 14; ++i, ++q) e[q % NC] += (uint64_t)x[i] * y[k - i];
+#pragma unroll
+        for (int i = k - 13; i < 14; ++i, ++q) e[q % NC] += (uint64_t)m[i] * kP29[k - i];
+        acc = e[0];
+#pragma unroll
+        for (int c = 1; c < NC; ++c) acc += e[c];
         o[k - 14] = (uint32_t)acc & kM29;
         acc >>= 29;
     }

@@ -40,6 +40,20 @@
 #include <cstdlib>
 #include <cstring>
 
+// Compile-time A/B switches of the one-root round kernel (round 4):
+// HB_SM_CACHE keeps the inbox loop's 32-sender mask word in registers,
+// HB_SM_MERGE takes a sender's Echo and EchoHash in one step.  Measured
+// (tools/sm_bench.py, one MI355X, ms per 5 rounds of 262,144 nodes, N=64 /
+// N=128): neither 0.670 / 1.368, merge 0.663 / 1.309, cache 0.690 / 1.470,
+// both 0.683 / 1.460 -- the cached word costs registers (more spills at 4
+// waves/SIMD) for LDS round trips the other waves were hiding.
+#ifndef HB_SM_CACHE
+#define HB_SM_CACHE 0
+#endif
+#ifndef HB_SM_MERGE
+#define HB_SM_MERGE 1
+#endif
+
 namespace hbrbc {
 
 namespace {
@@ -593,7 +607,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         m.drop = m.role == R_SILENT;
         const bool faker = a.fake_from[inst] == (uint8_t)me;
         for (int s = 0; s < n; ++s) {
-            m.em_focus(s >> 5);
+            if (HB_SM_CACHE) m.em_focus(s >> 5);
             if (s == me) continue;   // targets never include the sender
             const uint32_t cnt = inc(s);
             const uint32_t *rs = recs(s);
@@ -606,7 +620,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
                 // Echo to all but the right nodes, EchoHash to the right
                 // ones): this node handles at most one of them, so both are
                 // taken in one step through the merged handler.
-                if ((k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
+                if (HB_SM_MERGE && (k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
                     const uint32_t *r2 = r + (1 + W);
                     const uint32_t k1 = r2[0] & 0xFFu;
                     const bool hit2 = m.bit(r2 + 1, me);
@@ -671,7 +685,15 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
 // dependent read-modify-write chains (handle_echo: entry, Echo count, full
 // count, flags, outcome, ...) then cost LDS latency instead of an L2 round
 // trip each.  The state goes back at the end.
-template <bool ONE>
+// GREC (records in global memory): the state, outcomes and proofs are staged
+// as above, the records and counts are NOT -- a wave holds the nodes of one
+// instance (nodes a multiple of 64), so every record read is wave-uniform and
+// goes through the scalar unit (s_load, the scalar cache) straight from the
+// all-gathered inbox.  The LDS image shrinks to the state (N=128: 23 -> 13
+// KB per instance), so the grid's blocks fit the chip in one round instead of
+// 1.3 (a second, mostly idle round of blocks), and the per-thread staging
+// loop over the records (a chain of dependent global loads) goes away.
+template <bool ONE, bool GREC = false>
 __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, int f, int k,
                                                 int ipb) {
     extern __shared__ uint4 sm_lds4[];
@@ -686,8 +708,8 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
     // LDS: state [ipb][nodes * sb] | counts u32 [ipb][n] | records u32
     // [ipb][n][MR] | proof_ok [ipb][C * 2 * n] | decode_ok [ipb][C]
     const size_t o_cnt = (size_t)ipb * nodes * sb;   // sb % 8 == 0
-    const size_t o_rec = o_cnt + 4 * (size_t)ipb * n;
-    const size_t o_pok = o_rec + 4 * (size_t)ipb * n * MR;
+    const size_t o_rec = o_cnt + (GREC ? 0 : 4 * (size_t)ipb * n);
+    const size_t o_pok = o_rec + (GREC ? 0 : 4 * (size_t)ipb * n * MR);
     const size_t o_dok = o_pok + (size_t)ipb * C * 2 * n;
     uint8_t *gst = a.state + inst0 * nodes * sb;
     const size_t st_words = (size_t)ni * nodes * sb / 8;
@@ -695,7 +717,7 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
         reinterpret_cast<uint2 *>(lds)[i] = reinterpret_cast<const uint2 *>(gst)[i];
     uint32_t *lcnt = reinterpret_cast<uint32_t *>(lds + o_cnt);
     uint32_t *lrec = reinterpret_cast<uint32_t *>(lds + o_rec);
-    if (a.round > 0) {
+    if (!GREC && a.round > 0) {
         for (int i = tid; i < ni * n; i += T) {
             const int li = i / n, s = i - li * n;
             const uint32_t c = a.in_count[sm_in_block(a, inst0 + li, s)] & 0x7FFFFFFFu;
@@ -716,11 +738,26 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
     const int li = tid / (int)nodes, local = tid - li * (int)nodes;
     if (li < ni && (int)a.node_lo + local < n) {
         const size_t inst = inst0 + li;
-        const uint32_t *cb = lcnt + (size_t)li * n;
-        const uint32_t *rb = lrec + (size_t)li * n * MR;
-        sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
-                lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
-                [&](int s) { return cb[s]; }, [&](int s) { return rb + (size_t)s * MR; });
+        if constexpr (GREC) {
+            // one instance per wave: its inbox addresses are wave-uniform
+            const size_t ui = (size_t)__builtin_amdgcn_readfirstlane((int)li) + inst0;
+            const uint32_t *__restrict__ gin = a.in;
+            const uint32_t *__restrict__ gcnt = a.in_count;
+            sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local,
+                    lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
+                    lds + o_dok + (size_t)li * C,
+                    [&](int s) {
+                        const uint32_t c = gcnt[sm_in_block(a, ui, s)] & 0x7FFFFFFFu;
+                        return c < a.max_out ? c : a.max_out;
+                    },
+                    [&](int s) { return gin + sm_in_block(a, ui, s) * MR; });
+        } else {
+            const uint32_t *cb = lcnt + (size_t)li * n;
+            const uint32_t *rb = lrec + (size_t)li * n * MR;
+            sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
+                    lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
+                    [&](int s) { return cb[s]; }, [&](int s) { return rb + (size_t)s * MR; });
+        }
     }
     __syncthreads();
     for (size_t i = tid; i < st_words; i += T)
@@ -741,15 +778,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 sm_round_staged_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
     sm_round_staged<ONE>(a, n, f, k, ipb);
 }
+template <bool ONE>
+__global__ __launch_bounds__(256) void sm_round_grec_kernel(hbrbc_sm_args a, int n, int f, int k,
+                                                            int ipb) {
+    sm_round_staged<ONE, true>(a, n, f, k, ipb);
+}
+template <bool ONE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void
+sm_round_grec_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
+    sm_round_staged<ONE, true>(a, n, f, k, ipb);
+}
 
 }  // namespace
 
 // Launch plan: the staged form with ipb instances per workgroup (ipb x nodes
 // <= 256 threads, at most 128 unless one instance needs more) when its LDS
 // image fits 64 KiB; else the global form.
-static size_t sm_lds_bytes(const hbrbc_sm_args &a, int n, int ipb) {
+static size_t sm_lds_bytes(const hbrbc_sm_args &a, int n, int ipb, bool grec = false) {
     const size_t W = (n + 31) / 32, MR = (size_t)a.max_out * (1 + W);
-    const size_t per = a.nodes * sm_state_bytes(n, a.roots) + 4 * (size_t)n + 4 * (size_t)n * MR +
+    const size_t per = a.nodes * sm_state_bytes(n, a.roots) +
+                       (grec ? 0 : 4 * (size_t)n + 4 * (size_t)n * MR) +
                        (size_t)a.roots * 2 * n + a.roots;
     return ((size_t)ipb * per + 15) & ~(size_t)15;
 }
@@ -760,17 +808,23 @@ hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStrea
     const char *e = getenv("HBRBC_SM_STAGED");   // 0: the global form (A/B)
     const bool staged_ok = !(e && !strcmp(e, "0")) && a.nodes <= 256;
     int ipb = a.nodes >= 128 ? 1 : (int)(128 / a.nodes);
-    while (ipb > 1 && sm_lds_bytes(a, n, ipb) > 65536) --ipb;
-    if (staged_ok && sm_lds_bytes(a, n, ipb) <= 65536) {
+    // records through the scalar unit when every wave holds one instance's
+    // nodes (HBRBC_SM_GREC=0/1 forces, A/B)
+    const char *ge = getenv("HBRBC_SM_GREC");
+    const bool grec = (ge ? !strcmp(ge, "1") : true) && a.nodes % 64 == 0 && a.nodes >= 64;
+    while (ipb > 1 && sm_lds_bytes(a, n, ipb, grec) > 65536) --ipb;
+    if (staged_ok && sm_lds_bytes(a, n, ipb, grec) <= 65536) {
         const unsigned blocks = (unsigned)((a.count + ipb - 1) / ipb);
-        const size_t lds = sm_lds_bytes(a, n, ipb), threads_pb = (size_t)ipb * a.nodes;
+        const size_t lds = sm_lds_bytes(a, n, ipb, grec), threads_pb = (size_t)ipb * a.nodes;
         // waves per CU the LDS image allows (160 KiB per CU) above 3 per SIMD:
         // the 4-wave form (HBRBC_SM_W4=0/1 forces, A/B)
         const char *w4e = getenv("HBRBC_SM_W4");
         const bool w4 = w4e ? !strcmp(w4e, "1")
                             : (163840 / lds) * ((threads_pb + 63) / 64) > 12;
-        auto kern = a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true> : sm_round_staged_kernel<true>)
-                                 : (w4 ? sm_round_staged_w4_kernel<false> : sm_round_staged_kernel<false>);
+        auto kern = grec ? (a.roots == 1 ? (w4 ? sm_round_grec_w4_kernel<true> : sm_round_grec_kernel<true>)
+                                         : (w4 ? sm_round_grec_w4_kernel<false> : sm_round_grec_kernel<false>))
+                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true> : sm_round_staged_kernel<true>)
+                                         : (w4 ? sm_round_staged_w4_kernel<false> : sm_round_staged_kernel<false>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3((unsigned)threads_pb), lds, s, a, n, f, k, ipb);
         return hipGetLastError();
     }

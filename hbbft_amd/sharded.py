@@ -545,7 +545,7 @@ def rank_footprint(n, count, plen, world, rank=0, max_out=4, max_faults=4):
         "sm_output_root": G * C * R,
         "sm_faults": G * C * R * max(1, max_faults) * 2,
         "sm_fault_count": G * C * R * 4,
-        "sm_emitted": 8,
+        "sm_hist": 64 * 2 * 4,          # per round: records, overflow (max_rounds 64)
         "sm_inbox": G * G * C * R * max_out * (1 + W) * 4,
         "sm_inbox_count": G * G * C * R * 4,
     }

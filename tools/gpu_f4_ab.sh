@@ -7,9 +7,9 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 mkdir -p gpurun_out
 for L in ${LIBS:-libhbrbc.so}; do
   export HBRBC_LIB=$PWD/hbbft_amd/$L
-  timeout -k 10 300 python -u -m pytest tests/test_pairing.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/f4ab_tests_$L.log 2>&1
+  timeout -k 10 300 python -u -m pytest tests/test_pairing.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/f4ab_tests_$(basename $L).log 2>&1
   rc=$?; echo "$L tests exit $rc"; [ $rc -ne 0 ] && exit $rc
-  OUT=gpurun_out/f4ab_$L
+  OUT=gpurun_out/f4ab_$(basename $L)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- python3 tools/bench_pairing.py --prepared --n 262144 --reps 3 > $OUT.log 2>&1
   rc=$?; echo "$L bench exit $rc"; [ $rc -ne 0 ] && exit $rc
   tail -1 $OUT.log
