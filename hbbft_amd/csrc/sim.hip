@@ -53,6 +53,16 @@
 #ifndef HB_SM_MERGE
 #define HB_SM_MERGE 1
 #endif
+// Global-records kernel: HB_SM_CONSTAS reads the inbox through the constant
+// address space (wave-uniform reads become scalar loads), HB_SM_UREC also
+// fetches a record's recipient-mask words as scalar loads (each lane picks its
+// word) instead of one vector load per record.
+#ifndef HB_SM_CONSTAS
+#define HB_SM_CONSTAS 1
+#endif
+#ifndef HB_SM_UREC
+#define HB_SM_UREC 0
+#endif
 
 namespace hbrbc {
 
@@ -556,7 +566,7 @@ struct SmLayout {
 // Handles one node's inbox of the round (or, in round 0, the proposer's
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
 // `inc(s)` sender s's record count, `recs(s)` its records.
-template <bool ONE, class InCount, class Recs>
+template <bool ONE, bool UREC = false, class InCount, class Recs>
 __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
                         InCount inc, Recs recs) {
@@ -606,6 +616,23 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     } else {
         m.drop = m.role == R_SILENT;
         const bool faker = a.fake_from[inst] == (uint8_t)me;
+        // this node's bit in a record's recipient mask; with wave-uniform
+        // records (UREC) every mask word is a scalar load and the lane picks
+        // its word in registers (one scalar load each instead of a vector
+        // load per record)
+        const int mw = me >> 5;
+        auto rbit = [&](const uint32_t *r) -> bool {
+            if constexpr (UREC) {
+                uint32_t word = 0;
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t v = r[1 + w];
+                    word = w == mw ? v : word;
+                }
+                return (word >> (me & 31)) & 1u;
+            } else {
+                return m.bit(r + 1, me);
+            }
+        };
         for (int s = 0; s < n; ++s) {
             if (HB_SM_CACHE) m.em_focus(s >> 5);
             if (s == me) continue;   // targets never include the sender
@@ -614,17 +641,25 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
             for (uint32_t e = 0; e < cnt; ++e) {
                 const uint32_t *r = rs + (size_t)e * (1 + W);
                 const uint32_t k0 = r[0] & 0xFFu;
-                bool hit = m.bit(r + 1, me);
+                bool hit = rbit(r);
                 // An Echo and an EchoHash of the same sender in a row whose
                 // targets do not overlap at this node (handle_value emits
                 // Echo to all but the right nodes, EchoHash to the right
                 // ones): this node handles at most one of them, so both are
                 // taken in one step through the merged handler.
-                if (HB_SM_MERGE && (k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
+                // The step is taken only when every lane of the wave can take
+                // it (a sequential step is always exact), so the record index
+                // stays wave-uniform and the global-records kernel reads the
+                // records with scalar loads.
+                if (HB_SM_MERGE) {
+                    bool pair = false, hit2 = false;
                     const uint32_t *r2 = r + (1 + W);
-                    const uint32_t k1 = r2[0] & 0xFFu;
-                    const bool hit2 = m.bit(r2 + 1, me);
-                    if ((k1 == K_ECHO || k1 == K_ECHO_HASH) && k1 != k0 && !(hit && hit2)) {
+                    if ((k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
+                        const uint32_t k1 = r2[0] & 0xFFu;
+                        hit2 = rbit(r2);
+                        pair = (k1 == K_ECHO || k1 == K_ECHO_HASH) && k1 != k0 && !(hit && hit2);
+                    }
+                    if (__all(pair)) {
                         ++e;
                         if (hit2) {
                             r = r2;
@@ -741,16 +776,23 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
         if constexpr (GREC) {
             // one instance per wave: its inbox addresses are wave-uniform
             const size_t ui = (size_t)__builtin_amdgcn_readfirstlane((int)li) + inst0;
-            const uint32_t *__restrict__ gin = a.in;
-            const uint32_t *__restrict__ gcnt = a.in_count;
-            sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local,
+            // the constant address space: wave-uniform reads become s_load
+            // (the inbox is read-only during a round)
+#if HB_SM_CONSTAS
+            typedef __attribute__((address_space(4))) const uint32_t cu32;
+#else
+            typedef const uint32_t cu32;
+#endif
+            cu32 *gin = (cu32 *)a.in;
+            cu32 *gcnt = (cu32 *)a.in_count;
+            sm_node<ONE, HB_SM_UREC != 0>(a, n, f, k, inst * nodes + local, inst, local,
                     lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
                     lds + o_dok + (size_t)li * C,
                     [&](int s) {
                         const uint32_t c = gcnt[sm_in_block(a, ui, s)] & 0x7FFFFFFFu;
                         return c < a.max_out ? c : a.max_out;
                     },
-                    [&](int s) { return gin + sm_in_block(a, ui, s) * MR; });
+                    [&](int s) { return (const uint32_t *)(gin + sm_in_block(a, ui, s) * MR); });
         } else {
             const uint32_t *cb = lcnt + (size_t)li * n;
             const uint32_t *rb = lrec + (size_t)li * n * MR;
@@ -811,7 +853,11 @@ hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStrea
     // records through the scalar unit when every wave holds one instance's
     // nodes (HBRBC_SM_GREC=0/1 forces, A/B)
     const char *ge = getenv("HBRBC_SM_GREC");
-    const bool grec = (ge ? !strcmp(ge, "1") : true) && a.nodes % 64 == 0 && a.nodes >= 64;
+    // (N=64, 4096 instances: 0.64 ms LDS-staged vs 0.78 global; N=128, 2048
+    // instances: 1.37 vs 1.13-1.26 -- the LDS image only limits residency
+    // at N >= 128, tools/sm_bench.py, profiles/r4_sm_ab.jsonl)
+    const bool grec = (ge ? !strcmp(ge, "1") : a.nodes >= 128) && a.nodes % 64 == 0 &&
+                      a.nodes >= 64;
     while (ipb > 1 && sm_lds_bytes(a, n, ipb, grec) > 65536) --ipb;
     if (staged_ok && sm_lds_bytes(a, n, ipb, grec) <= 65536) {
         const unsigned blocks = (unsigned)((a.count + ipb - 1) / ipb);
