@@ -76,6 +76,9 @@ def parse():
                     help="with --streams > 1: each sub-batch starts after the previous one's encode")
     ap.add_argument("--no-leaf-reuse", action="store_true",
                     help="skip the instance-mode leaf_reuse variant (labelled, not the headline)")
+    ap.add_argument("--no-sm-overlap", action="store_true",
+                    help="validator mode on one rank: run each step's state machine after its "
+                         "decode instead of beside the next step's data plane")
     ap.add_argument("--vsubs", type=int, default=4,
                     help="validator mode with >1 rank: pipelined sub-batches per step")
     ap.add_argument("--mode", choices=["instances", "validators", "both"], default="both",
@@ -583,11 +586,15 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     import torch.distributed as dist
 
     from hbbft_amd.sharded import (CommTimer, DistExchange, ShardedBroadcast, SoloExchange,
-                                   pipelined_step)
+                                   overlapped_steps, pipelined_step)
 
     nsub = max(1, min(args.vsubs, count)) if world > 1 else 1
+    # one rank: the state machine of step i on a side stream beside the data
+    # plane of step i + 1 (two state-machine slots)
+    overlap = world == 1 and not args.no_sm_overlap
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
-    subs = [ShardedBroadcast(n, bounds[i + 1] - bounds[i], plen, rank, world, device=local)
+    subs = [ShardedBroadcast(n, bounds[i + 1] - bounds[i], plen, rank, world, device=local,
+                             sm_slots=2 if overlap else 1)
             for i in range(nsub)]
     sb = subs[0]
     ex = DistExchange() if world > 1 else SoloExchange()
@@ -597,14 +604,22 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     pay_sub = [gen_payloads(torch, SEED, rank * count + bounds[i], bounds[i + 1] - bounds[i], plen,
                             pstride, dev) for i in range(nsub)]
 
+    side = torch.cuda.Stream(dev) if overlap else None
+
     def step():
         if world > 1:   # sub-batches with every exchange in flight behind compute
             pipelined_step(subs, pay_sub, ex, timer)
         else:
             sb.step(pay_sub[0], ex)
 
-    for _ in range(args.warmup):
-        step()
+    def run_steps(k, timing=None):
+        if overlap:
+            overlapped_steps(sb, pay_sub[0], ex, k, side, timing)
+        else:
+            for _ in range(k):
+                step()
+
+    run_steps(args.warmup)
     torch.cuda.synchronize(dev)
     if not args.no_verify:
         for i, s_ in enumerate(subs):
@@ -628,15 +643,18 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    sm_side = [] if overlap else None
+    run_steps(args.steps, sm_side)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     for s_ in subs:
         s_.rb.profile(False)
-    sm_ms = sum(e0.elapsed_time(e1) for e0, e1 in sb.sm_timing) / args.steps
+    if overlap:   # spans on the side stream, beside the next step's data plane
+        sm_ms = sum(e0.elapsed_time(e1) for e0, e1 in sm_side) / args.steps
+    else:
+        sm_ms = sum(e0.elapsed_time(e1) for e0, e1 in sb.sm_timing) / args.steps
     sb.sm_timing = None
     elapsed = max_over_ranks(elapsed, world, dev)
     xms = timer.elapsed_ms() / args.steps if world > 1 else 0.0
@@ -691,21 +709,28 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                    # per-rank device bytes of this object at 1/2/4/8 GPUs (rank 0;
                    # hbbft_amd.sharded.rank_footprint, torch buffers + reconstruct
                    # workspace bound), against 288 GB of HBM per MI355X
-                   "hbm_footprint_per_rank": footprint_summary(n, count, plen)},
+                   "hbm_footprint_per_rank": footprint_summary(n, count, plen,
+                                                               2 if overlap else 1)},
         "exchange": {"ms_per_step": xms, "bytes_per_step_per_gpu": xbytes,
                      "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
                      "backend": ex.backend, "per_rank": per_rank},
         "work_per_step_rank0": counts,
         "stages_ms_per_step": dict({s: stages[s][0] / args.steps for s in stages},
-                                   state_machine=sm_ms),
+                                   **({"state_machine_overlapped": sm_ms} if overlap
+                                      else {"state_machine": sm_ms})),
+        "state_machine_schedule": ("step i's rounds on a second HIP stream beside step i + 1's "
+                                   "data plane (two state-machine slots); every step's rounds "
+                                   "complete inside the timed region" if overlap else
+                                   "after each step's decode, in lockstep over the ranks"),
     }
 
 
-def footprint_summary(n, count, plen):
+def footprint_summary(n, count, plen, sm_slots=1):
     from hbbft_amd.sharded import HBM_PER_GPU, rank_footprint
     out = {}
     for g in (1, 2, 4, 8):
-        fp = rank_footprint(n, count, plen, g, 0)
+        # (two state-machine slots only where they are used: one rank)
+        fp = rank_footprint(n, count, plen, g, 0, sm_slots=sm_slots if g == 1 else 1)
         out["G%d" % g] = {"bytes": fp["total_bytes"], "frac_of_288GB": fp["frac_of_hbm"],
                           "echo_slab_bytes": fp["buffers"].get("echo_sh", fp["buffers"]["slab"])}
     assert all(v["bytes"] < HBM_PER_GPU for v in out.values()), out

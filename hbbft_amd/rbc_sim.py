@@ -354,50 +354,100 @@ def _check_batch(ranks, h, r0, own=None):
     return None
 
 
+class LocalRounds:
+    """The rounds of the StateMachineRank objects of one process with no
+    process group -- the virtual ranks of a loopback topology (loopback=True:
+    their records are gathered between rounds) or independent objects each
+    talking to itself -- split into enqueue and read-back so a caller can
+    overlap them with other work: `launch()` enqueues the first ROUND_BATCH
+    rounds on `stream` (default: the current stream) and returns at once;
+    `wait()` reads the per-round counts back (one host read, synchronising
+    that stream only), enqueues and reads further batches until the network
+    is quiescent, and returns the number of rounds.
+
+    Round r gets the device total of round r - 1's records as `active` and
+    returns at once when it is 0, so the rounds past quiescence cost an empty
+    launch (round 3 read the counts back after every round: ~0.3 ms of host
+    gaps per step in the validator-sharded bench objects)."""
+
+    def __init__(self, ranks, loopback, max_rounds=64, stream=None):
+        self.ranks = ranks
+        self.max_rounds = min(max_rounds, min(sm.max_rounds for sm in ranks))
+        self.loop = LoopbackExchange(ranks) if loopback and len(ranks) > 1 else None
+        self.stream = stream
+        dev = ranks[0].device
+        # with a loopback the next round's flag is the total over all ranks
+        self.act = torch.zeros(self.max_rounds + 1, dtype=torch.int32, device=dev) \
+            if self.loop is not None else None
+        self.next = 0
+
+    def _enqueue(self, r, hi):
+        ranks, act = self.ranks, self.act
+        for rr in range(r, hi):
+            for sm in ranks:
+                if rr == 0:
+                    sm.round(0)
+                else:   # own count (independent objects) or the device total
+                    sm.round(rr, active=sm.emitted(rr - 1) if act is None else act[rr])
+            if act is not None:
+                act[rr + 1].copy_(torch.stack([sm.emitted(rr) for sm in ranks]).sum())
+            if self.loop is not None:
+                self.loop.gather()
+            else:
+                for sm in ranks:
+                    sm.swap_local()
+        self.next = hi
+
+    def _ctx(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
+
+    def launch(self, fresh=True):
+        with self._ctx():
+            if fresh:
+                for sm in self.ranks:
+                    sm.reset()
+            self._enqueue(0, min(self.max_rounds, ROUND_BATCH))
+        return self
+
+    def wait(self):
+        r = 0   # first round whose count has not been read
+        with self._ctx():
+            while True:
+                hi = self.next
+                h = torch.stack([sm.hist[r:hi] for sm in self.ranks]).cpu()   # one read
+                done = _check_batch(self.ranks, h, r)
+                if done is not None:
+                    return done
+                if hi >= self.max_rounds:
+                    raise RuntimeError("state machine did not quiesce in %d rounds"
+                                       % self.max_rounds)
+                self._enqueue(hi, min(self.max_rounds, hi + ROUND_BATCH))
+                r = hi
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
     """Drive the state machine until no node emits a message.  `ranks`: the
     StateMachineRank objects of this process -- all virtual ranks of one
     topology for a loopback run (exchange None), or independent objects of
     this rank (e.g. pipelined sub-batches) with a DistExchange / SoloExchange
-    `exchange`, whose world they share.  Returns the number of rounds.
-
-    Rounds go out ROUND_BATCH at a time with no host read in between: round r
-    gets the device total of round r - 1's records as `active`, and returns
-    at once when it is 0, so the rounds past quiescence cost an empty launch;
-    one read of the per-round counts per batch finds the quiescent round
-    (round 3 read them back after every round: ~0.3 ms of host gaps per step
-    in the validator-sharded bench objects)."""
-    max_rounds = min(max_rounds, min(sm.max_rounds for sm in ranks))
-    if fresh:
-        for sm in ranks:
-            sm.reset()
+    `exchange`, whose world they share.  Returns the number of rounds
+    (LocalRounds / _run_rounds_dist: batches of rounds, one read-back per
+    batch)."""
     if exchange is not None and exchange.world > 1:
-        return _run_rounds_dist(ranks, exchange, max_rounds)
-    loop = LoopbackExchange(ranks) if exchange is None and len(ranks) > 1 else None
-    dev = ranks[0].device
-    act = torch.zeros(max_rounds + 1, dtype=torch.int32, device=dev) if len(ranks) > 1 else None
-    r = 0
-    while r < max_rounds:
-        hi = min(max_rounds, r + ROUND_BATCH)
-        for rr in range(r, hi):
+        max_rounds = min(max_rounds, min(sm.max_rounds for sm in ranks))
+        if fresh:
             for sm in ranks:
-                if rr == 0:
-                    sm.round(0)
-                else:   # one rank: its own count; several: their device total
-                    sm.round(rr, active=sm.emitted(rr - 1) if act is None else act[rr])
-            if act is not None:
-                act[rr + 1].copy_(torch.stack([sm.emitted(rr) for sm in ranks]).sum())
-            if loop is not None:
-                loop.gather()
-            else:
-                for sm in ranks:
-                    sm.swap_local()
-        h = torch.stack([sm.hist[r:hi] for sm in ranks]).cpu()     # one read per batch
-        done = _check_batch(ranks, h, r)
-        if done is not None:
-            return done
-        r = hi
-    raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
+                sm.reset()
+        return _run_rounds_dist(ranks, exchange, max_rounds)
+    return LocalRounds(ranks, loopback=exchange is None, max_rounds=max_rounds).launch(fresh).wait()
 
 
 def _run_rounds_dist(ranks, ex, max_rounds):

@@ -242,7 +242,7 @@ class ShardedBroadcast:
     """The per-rank state of the validator-sharded simulation: `count` local
     proposals of `plen` bytes per step on `device`."""
 
-    def __init__(self, n, count, plen, rank, world, device=0, specialise=True):
+    def __init__(self, n, count, plen, rank, world, device=0, specialise=True, sm_slots=1):
         self.topo = t = Topology(n, world)
         self.rank, self.world, self.count, self.plen = rank, world, count, plen
         self.rb = rb = RbcBatch(n, t.f, device=device)
@@ -308,11 +308,17 @@ class ShardedBroadcast:
         # validator proposers(s, C)[i]
         from .rbc_sim import StateMachineRank, honest_tensors
         props = [p_ for s_ in range(G) for p_ in t.proposers(s_, C)]
-        self.sm_ok = torch.zeros((G * C, 1, 2, n), dtype=torch.uint8, device=dev)
-        self.sm_dec = torch.zeros((G * C, 1), dtype=torch.uint8, device=dev)
-        self.sm = StateMachineRank(n, G * C, 1, honest_tensors(n, props, dev), rank, world,
-                                   device=device, max_out=4, max_faults=4, ok=self.sm_ok,
-                                   dec=self.sm_dec)
+        # sm_slots = 2: two state machines with their own outcome buffers, so
+        # the rounds of step i (a side stream) can run while step i + 1's data
+        # plane fills the other slot's outcomes (overlapped_steps)
+        sc = honest_tensors(n, props, dev)
+        self.sms = []
+        for _ in range(sm_slots):
+            ok = torch.zeros((G * C, 1, 2, n), dtype=torch.uint8, device=dev)
+            dec = torch.zeros((G * C, 1), dtype=torch.uint8, device=dev)
+            self.sms.append(StateMachineRank(n, G * C, 1, sc, rank, world, device=device,
+                                             max_out=4, max_faults=4, ok=ok, dec=dec))
+        self.slot = 0
         self.sm_rounds = 0
         self.sm_timing = None   # a list: (start, end) events of every run_state_machines
         self.own_cols = torch.tensor([j - rank * R for j in own] or [0], dtype=torch.int64,
@@ -424,6 +430,11 @@ class ShardedBroadcast:
                             self.plen_out, self.status, known_leaves=True)
         self.thresholds()
 
+    @property
+    def sm(self):
+        """The state machine of the current slot."""
+        return self.sms[self.slot]
+
     def thresholds(self):
         """Inputs of the state machine from this step's data plane: proof (0,
         j) of every instance validates iff validator j's Value did (the Echo
@@ -436,8 +447,8 @@ class ShardedBroadcast:
         valid = self.okv_all.transpose(0, 1).reshape(G * C, t.npad)[:, : t.n]
         torch.sum(valid, dim=1, dtype=torch.int32, out=self.echo_senders)
         torch.sum(self.present, dim=1, dtype=torch.int32, out=self.full_echos)
-        self.sm_ok[:, 0, 0, :].copy_(valid)
-        self.sm_dec[:, 0].copy_(self.status == 0)
+        self.sm.ok[:, 0, 0, :].copy_(valid)
+        self.sm.dec[:, 0].copy_(self.status == 0)
 
     def finish(self):
         """After the state machine's rounds: decided[i] = every validator this
@@ -450,7 +461,9 @@ class ShardedBroadcast:
     def state_machine(self, ex):
         self.sm_rounds = run_state_machines([self], ex)
 
-    def step(self, payloads, ex):
+    def data_step(self, payloads, ex):
+        """Propose, exchange, validate and decode (the data plane of a step);
+        the decode leaves the state machine's outcomes in the current slot."""
         self.propose(payloads)
         self.pack_value()
         self.exchange_value(ex)
@@ -458,6 +471,9 @@ class ShardedBroadcast:
         self.exchange_echo(ex)
         self.validate_echoes()
         self.decode()
+
+    def step(self, payloads, ex):
+        self.data_step(payloads, ex)
         self.state_machine(ex)
 
     # accounting --------------------------------------------------------------
@@ -484,7 +500,7 @@ class ShardedBroadcast:
 HBM_PER_GPU = 288 * 10**9   # MI355X HBM3E
 
 
-def rank_footprint(n, count, plen, world, rank=0, max_out=4, max_faults=4):
+def rank_footprint(n, count, plen, world, rank=0, max_out=4, max_faults=4, sm_slots=1):
     """Device bytes one rank's ShardedBroadcast(n, count, plen, rank, world)
     allocates, by buffer, without a GPU: the torch tensors of __init__ (and
     of its StateMachineRank) at their exact shapes, aliases at world 1
@@ -531,23 +547,23 @@ def rank_footprint(n, count, plen, world, rank=0, max_out=4, max_faults=4):
         "echo_senders": G * C * 4,
         "full_echos": G * C * 4,
         "decided": G * C,
-        "sm_ok": G * C * 2 * n,
-        "sm_dec": G * C,
+        "sm_ok": sm_slots * G * C * 2 * n,
+        "sm_dec": sm_slots * G * C,
         "own_cols": max(1, len(own)) * 8,
         "own_rows": max(1, len(own)) * 8,
         "echo_cols": max(1, len(echo)) * 8,
         # StateMachineRank (rbc_sim.py) of G * C instances, honest scenario
         # (honest_tensors: role / value_root / value_tamper share one [cnt][n])
         "sm_scenario": G * C * (1 + n + 2) + G * C * W * 4,
-        "sm_state": G * C * R * sm_state,
-        "sm_out": G * C * R * max_out * (1 + W) * 4,
-        "sm_out_count": G * C * R * 4,
-        "sm_output_root": G * C * R,
-        "sm_faults": G * C * R * max(1, max_faults) * 2,
-        "sm_fault_count": G * C * R * 4,
-        "sm_hist": 64 * 2 * 4,          # per round: records, overflow (max_rounds 64)
-        "sm_inbox": G * G * C * R * max_out * (1 + W) * 4,
-        "sm_inbox_count": G * G * C * R * 4,
+        "sm_state": sm_slots * (G * C * R * sm_state),
+        "sm_out": sm_slots * (G * C * R * max_out * (1 + W) * 4),
+        "sm_out_count": sm_slots * (G * C * R * 4),
+        "sm_output_root": sm_slots * (G * C * R),
+        "sm_faults": sm_slots * (G * C * R * max(1, max_faults) * 2),
+        "sm_fault_count": sm_slots * (G * C * R * 4),
+        "sm_hist": sm_slots * (64 * 2 * 4),          # per round: records, overflow (max_rounds 64)
+        "sm_inbox": sm_slots * (G * G * C * R * max_out * (1 + W) * 4),
+        "sm_inbox_count": sm_slots * (G * G * C * R * 4),
     }
     if G > 1:
         b.update({"recv_sh": G * C * R * stride, "recv_dg": G * C * R * dsz,
@@ -599,6 +615,52 @@ def pipelined_step(subs, payloads, ex, timer):
     rounds = run_state_machines(subs, ex)
     for sb in subs:
         sb.sm_rounds = rounds
+
+
+def overlapped_steps(sb, payloads, ex, steps, side, timing=None):
+    """`steps` steps of one rank with no process group (world 1), the state
+    machine of step i on the `side` stream overlapping the data plane of step
+    i + 1 on the current stream (sb built with sm_slots=2; the slots
+    alternate).  The rounds are latency-bound at low occupancy, the data
+    plane issue-bound: run side by side the GPU fills the one's idle issue
+    slots with the other's work.  Every step's rounds have completed (and
+    sb.decided holds the last step's flags) when this returns; `timing`: a
+    list that receives (start, end) events of each step's rounds on the side
+    stream."""
+    from .rbc_sim import LocalRounds
+    assert len(sb.sms) == 2 and ex.world == 1
+    cur = torch.cuda.current_stream()
+    pending = None
+
+    def drain(p):
+        slot, lr, ev = p
+        rounds = lr.wait()
+        prev = sb.slot
+        sb.slot = slot
+        with torch.cuda.stream(side):
+            sb.finish()
+            if ev is not None:
+                ev[1].record()
+        sb.slot = prev
+        sb.sm_rounds = rounds
+
+    for i in range(steps):
+        sb.slot = i % 2
+        sb.data_step(payloads, ex)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        if pending is not None:
+            drain(pending)          # host read of step i - 1's rounds, step i queued
+        side.wait_event(ready)
+        ev = None
+        if timing is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(side)
+            timing.append(ev)
+        pending = (sb.slot, LocalRounds([sb.sm], loopback=False, stream=side).launch(), ev)
+    if pending is not None:
+        drain(pending)
+    cur.wait_stream(side)
 
 
 def run_state_machines(subs, ex):
