@@ -461,6 +461,27 @@ class ShardedBroadcast:
     def state_machine(self, ex):
         self.sm_rounds = run_state_machines([self], ex)
 
+    def encode_phase(self, payloads):
+        """The proposer's frame + encode (the first kernel of a step)."""
+        rb, C = self.rb, self.count
+        st, rpb, bst, ist = self._prop_layout()
+        rb.frame_encode_rows(payloads, self.plen, self.slab, C, st, rpb, bst, ist)
+
+    def rest_phase(self, ex):
+        """Everything of a step after the encoder: tree, proofs, exchanges,
+        validation, decode (which leaves the state machine's outcomes in the
+        current slot)."""
+        rb, S, C = self.rb, self.S, self.count
+        st, rpb, bst, ist = self._prop_layout()
+        rb.merkle_rows(self.slab, S, C, st, rpb, bst, ist, self.nodes)
+        rb.proofs(self.nodes, self.digests, self.ndig)
+        self.pack_value()
+        self.exchange_value(ex)
+        self.validate_values()
+        self.exchange_echo(ex)
+        self.validate_echoes()
+        self.decode()
+
     def data_step(self, payloads, ex):
         """Propose, exchange, validate and decode (the data plane of a step);
         the decode leaves the state machine's outcomes in the current slot."""
@@ -619,18 +640,31 @@ def pipelined_step(subs, payloads, ex, timer):
 
 def overlapped_steps(sb, payloads, ex, steps, side, timing=None):
     """`steps` steps of one rank with no process group (world 1), the state
-    machine of step i on the `side` stream overlapping the data plane of step
+    machine of step i on the `side` stream beside the data plane of step
     i + 1 on the current stream (sb built with sm_slots=2; the slots
     alternate).  The rounds are latency-bound at low occupancy, the data
-    plane issue-bound: run side by side the GPU fills the one's idle issue
-    slots with the other's work.  Every step's rounds have completed (and
-    sb.decided holds the last step's flags) when this returns; `timing`: a
-    list that receives (start, end) events of each step's rounds on the side
-    stream."""
+    plane's sponges issue-bound: side by side the GPU fills the one's idle
+    issue slots with the other's work.  Step i's rounds start after step
+    i + 1's encoder: the LDS-staged encoder needs 48 KB of LDS per workgroup
+    and ran at half speed beside the rounds' LDS images (validator cfg4:
+    encode 0.69 -> 1.50 ms), the sponge kernels use none.  Every step's
+    rounds have completed (and sb.decided holds the last step's flags) when
+    this returns; `timing`: a list that receives (start, end) events of each
+    step's rounds on the side stream."""
     from .rbc_sim import LocalRounds
     assert len(sb.sms) == 2 and ex.world == 1
     cur = torch.cuda.current_stream()
-    pending = None
+
+    def launch(slot, ready, after):
+        side.wait_event(ready)
+        if after is not None:
+            side.wait_event(after)
+        ev = None
+        if timing is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(side)
+            timing.append(ev)
+        return slot, LocalRounds([sb.sms[slot]], loopback=False, stream=side).launch(), ev
 
     def drain(p):
         slot, lr, ev = p
@@ -644,22 +678,23 @@ def overlapped_steps(sb, payloads, ex, steps, side, timing=None):
         sb.slot = prev
         sb.sm_rounds = rounds
 
+    prev_ready = None   # step i - 1's data plane is done (its outcomes are in)
     for i in range(steps):
         sb.slot = i % 2
-        sb.data_step(payloads, ex)
-        ready = torch.cuda.Event()
-        ready.record(cur)
-        if pending is not None:
-            drain(pending)          # host read of step i - 1's rounds, step i queued
-        side.wait_event(ready)
-        ev = None
-        if timing is not None:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record(side)
-            timing.append(ev)
-        pending = (sb.slot, LocalRounds([sb.sm], loopback=False, stream=side).launch(), ev)
-    if pending is not None:
-        drain(pending)
+        sb.encode_phase(payloads)
+        after_encode = torch.cuda.Event()
+        after_encode.record(cur)
+        running = None
+        if prev_ready is not None:   # step i - 1's rounds, after step i's encoder
+            running = launch((i - 1) % 2, prev_ready, after_encode)
+        sb.rest_phase(ex)
+        prev_ready = torch.cuda.Event()
+        prev_ready.record(cur)
+        if running is not None:
+            drain(running)           # host read; step i's data plane is queued
+    if prev_ready is not None:
+        drain(launch((steps - 1) % 2, prev_ready, None))
+    sb.slot = (steps - 1) % 2
     cur.wait_stream(side)
 
 
