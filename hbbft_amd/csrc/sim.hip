@@ -855,7 +855,7 @@ hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStrea
     const char *ge = getenv("HBRBC_SM_GREC");
     // (N=64, 4096 instances: 0.64 ms LDS-staged vs 0.78 global; N=128, 2048
     // instances: 1.37 vs 1.13-1.26 -- the LDS image only limits residency
-    // at N >= 128, tools/sm_bench.py, profiles/r4_sm_ab.jsonl)
+    // at N >= 128, tools/sm_bench.py, profiles/r4_sm_ab.txt)
     const bool grec = (ge ? !strcmp(ge, "1") : a.nodes >= 128) && a.nodes % 64 == 0 &&
                       a.nodes >= 64;
     while (ipb > 1 && sm_lds_bytes(a, n, ipb, grec) > 65536) --ipb;
