@@ -230,6 +230,10 @@ __device__ __forceinline__ void unframe_put(uint8_t *pb, uint32_t S, uint32_t ro
         *reinterpret_cast<hb_u32x4_a1 *>(pb + dst) = (hb_u32x4_a1){a, b, c, d};
 }
 
+__device__ __forceinline__ uint32_t rfl(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 template <int RT, int MODE>
 // Workgroup = up to 4 waves over the SAME 2048 positions; wave w produces
 // passes w, w + nwaves, ...  The waves read identical input bytes at the
@@ -237,7 +241,12 @@ template <int RT, int MODE>
 // its passes one after another re-read every input per pass: 3x the HBM/MALL
 // traffic at m = 42).  Instance i uses the coefficients and row lists of
 // slot pat[i] (the decode-matrix cache) or of slot i / the shared slot 0.
-__global__ __launch_bounds__(256) void gf_bitslice_kernel(
+#ifdef HB_GF_WPE   // A/B: waves per SIMD the register budget is cut to
+#define HB_GF_ATTR __attribute__((amdgpu_waves_per_eu(HB_GF_WPE)))
+#else
+#define HB_GF_ATTR
+#endif
+__global__ __launch_bounds__(256) HB_GF_ATTR void gf_bitslice_kernel(
     uint8_t *__restrict__ base, size_t inst_stride, RowMap rows, uint32_t row_bytes,
     const uint8_t *__restrict__ coefs, size_t coef_slot_stride,
     const uint32_t *__restrict__ in_idx, size_t in_idx_stride,
@@ -386,6 +395,141 @@ __global__ __launch_bounds__(256) void gf_bitslice_kernel(
                 }
             }
         };
+        if constexpr (MODE == 4) {
+            // Two inputs per step (j, j + 1): each keeps its own rotating
+            // doubling, so plane q of 2^b x_j and of 2^b x_j+1 sit in fixed
+            // registers side by side and, when bit b of both coefficients is
+            // set, one v_xor3 per plane folds both into the accumulator: 6
+            // instead of 8 VALU per (row, bit) on average.  (MODE 3 paired
+            // two bits of ONE coefficient, whose multiples share registers:
+            // copies and 3-way scalar dispatch cost more than it saved.)
+            // A missing second input (odd nin) gets coefficient 0: no bit set.
+            // A/B (HBRBC_GF=bitslice_x2, rejected): VALU -18 % (1.91 vs 2.32 G
+            // per launch) but SALU + branches +33 % (three scalar tests per bit
+            // and pair; a nested if / else went back to lane-mask flow blocks
+            // and v_mov copies), 115 VGPRs = 4 waves/SIMD instead of 5, and a
+            // wave issues one instruction per 4 cycles whatever its kind: the
+            // same instruction count per wave, 3.50 vs 3.15 ms at cfg3.
+            auto consume2 = [&](uint32_t ra, const uint4 &cwa, const uint4 &la, const uint4 &ha_,
+                                uint32_t rb, const uint4 &cwb, const uint4 &lb, const uint4 &hb_,
+                                bool two) {
+                const uint4 ha = full ? ha_ : make_uint4(0, 0, 0, 0);
+                const uint4 hb = full ? hb_ : make_uint4(0, 0, 0, 0);
+                if (ufp && p == 0 && active) {
+                    if (ra < uf_k) {
+                        unframe_put(ufp, uf_S, ra, off, la.x, la.y, la.z, la.w);
+                        if (full) unframe_put(ufp, uf_S, ra, off + d2, ha.x, ha.y, ha.z, ha.w);
+                    }
+                    if (two && rb < uf_k) {
+                        unframe_put(ufp, uf_S, rb, off, lb.x, lb.y, lb.z, lb.w);
+                        if (full) unframe_put(ufp, uf_S, rb, off + d2, hb.x, hb.y, hb.z, hb.w);
+                    }
+                }
+                uint32_t xa[8] = {la.x, la.y, la.z, la.w, ha.x, ha.y, ha.z, ha.w};
+                uint32_t xb[8] = {lb.x, lb.y, lb.z, lb.w, hb.x, hb.y, hb.z, hb.w};
+                bs_transpose(xa);
+                bs_transpose(xb);
+                // wave-uniform: keep the bit tests on the scalar unit
+                const uint32_t keep = 0u - (uint32_t)two;
+                const uint32_t ca[4] = {rfl(cwa.x), rfl(cwa.y), rfl(cwa.z), rfl(cwa.w)};
+                const uint32_t cb[4] = {rfl(cwb.x & keep), rfl(cwb.y & keep), rfl(cwb.z & keep),
+                                        rfl(cwb.w & keep)};
+                // per coefficient bit: both inputs / only the first / only the second
+                uint32_t both[4], oa[4], ob[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    both[w] = ca[w] & cb[w];
+                    oa[w] = ca[w] & ~cb[w];
+                    ob[w] = cb[w] & ~ca[w];
+                }
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+#pragma unroll
+                    for (int t = 0; t < RT; ++t) {
+                        const int sh = 8 * (t & 3) + b;
+                        // three one-sided uniform branches on scalar bits (an if /
+                        // else chain left the structurizer's flow blocks with v_mov
+                        // copies, and && of two bits became lane-mask arithmetic)
+                        if ((both[t >> 2] >> sh) & 1u) {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q)
+                                acc[t][q] = xor3(acc[t][q], xa[(q - b) & 7], xb[(q - b) & 7]);
+                        }
+                        if ((oa[t >> 2] >> sh) & 1u) {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) acc[t][q] ^= xa[(q - b) & 7];
+                        }
+                        if ((ob[t >> 2] >> sh) & 1u) {
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) acc[t][q] ^= xb[(q - b) & 7];
+                        }
+                    }
+                    if (b < 7) {
+                        const uint32_t h = xa[(7 - b) & 7], g = xb[(7 - b) & 7];
+                        xa[(1 - b) & 7] ^= h;
+                        xa[(2 - b) & 7] ^= h;
+                        xa[(3 - b) & 7] ^= h;
+                        xb[(1 - b) & 7] ^= g;
+                        xb[(2 - b) & 7] ^= g;
+                        xb[(3 - b) & 7] ^= g;
+                    }
+                }
+            };
+            // the same software pipeline as below, one PAIR of inputs per
+            // half-step: pair (j + 2, j + 3) in flight while pair j is consumed
+            uint32_t ra0 = row_of(0), ra1 = row_of(1), rb0 = row_of(2), rb1 = row_of(3);
+            uint4 ca0 = coef_of(0), ca1 = coef_of(1), cb0, cb1;
+            uint32_t orows[RT];
+#pragma unroll
+            for (int t = 0; t < RT; ++t) orows[t] = oidx[p * RT + t < nout ? p * RT + t : nout - 1];
+            uint4 a0l, a0h, a1l, a1h, b0l = make_uint4(0, 0, 0, 0), b0h = b0l, b1l = b0l, b1h = b0l;
+            load_row(ra0, a0l, a0h);
+            load_row(ra1, a1l, a1h);
+            for (int j = 0; j < nin; j += 4) {
+                __asm__ volatile("" ::"s"(rb0), "s"(rb1), "s"(ca0.x), "s"(ca0.y), "s"(ca0.z),
+                                 "s"(ca0.w), "s"(ca1.x), "s"(ca1.y), "s"(ca1.z), "s"(ca1.w)
+                                 : "memory");
+                load_row(rb0, b0l, b0h);
+                load_row(rb1, b1l, b1h);
+                const uint32_t rn0 = row_of(j + 4), rn1 = row_of(j + 5);
+                cb0 = coef_of(j + 2);
+                cb1 = coef_of(j + 3);
+                consume2(ra0, ca0, a0l, a0h, ra1, ca1, a1l, a1h, j + 1 < nin);
+                __asm__ volatile("" ::"s"(rn0), "s"(rn1), "s"(cb0.x), "s"(cb0.y), "s"(cb0.z),
+                                 "s"(cb0.w), "s"(cb1.x), "s"(cb1.y), "s"(cb1.z), "s"(cb1.w)
+                                 : "memory");
+                load_row(rn0, a0l, a0h);
+                load_row(rn1, a1l, a1h);
+                const uint32_t rn2 = row_of(j + 6), rn3 = row_of(j + 7);
+                ca0 = coef_of(j + 4);
+                ca1 = coef_of(j + 5);
+                if (j + 2 < nin)
+                    consume2(rb0, cb0, b0l, b0h, rb1, cb1, b1l, b1h, j + 3 < nin);
+                ra0 = rn0;
+                ra1 = rn1;
+                rb0 = rn2;
+                rb1 = rn3;
+            }
+            if (active) {
+#pragma unroll
+                for (int t = 0; t < RT; ++t) {
+                    if (p * RT + t < nout) {
+                        bs_transpose(acc[t]);
+                        const uint32_t orow = orows[t];
+                        uint8_t *dst = ib + rows.off(orow) + off;
+                        store16_stream(dst, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+                        if (full) store16_stream(dst + d2, acc[t][4], acc[t][5], acc[t][6], acc[t][7]);
+                        if (ufp && orow < uf_k) {
+                            unframe_put(ufp, uf_S, orow, off, acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+                            if (full)
+                                unframe_put(ufp, uf_S, orow, off + d2, acc[t][4], acc[t][5], acc[t][6],
+                                            acc[t][7]);
+                        }
+                    }
+                }
+            }
+            continue;
+        }
         // Software pipeline, unrolled by two so no register ever moves: the 32
         // input bytes of j+1 are in flight (buffer B) while input j (buffer A)
         // is consumed, and vice versa.  The scalar operands run one input
@@ -558,6 +702,44 @@ __global__ __launch_bounds__(kBlock) void leaf_hash_list_pl_kernel(
     if (g >= *counter) return;   // both lanes of a pair leave together
     const uint2 e = list[g];
     uint32_t d[8];
+    sha3_256_row_pl(shards + e.x * inst_stride + rows.off(e.y), S, h, d);
+    if (!h) store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
+}
+
+// The same list balanced over the SIMDs.  A sponge is a serial chain, so a
+// list is as slow as its busiest SIMD: 86,016 sponges (validator cfg3 / cfg4)
+// are 84 per SIMD -- 1.3 one-lane waves, i.e. two waves of 4,395 VALU per
+// permutation back to back on a quarter of the SIMDs, or 2.6 pair-lane waves
+// rounded up to three of ~2,950.  Here one 512-lane block per CU (8 waves, two
+// per SIMD) takes an equal share of the list: whole rounds of 256 sponges on
+// waves 0-3, one lane each, and a remainder of at most 128 on waves 4-7, two
+// lanes each (a larger remainder is one more one-lane round).  At 84 per SIMD
+// a SIMD then runs one wave of each form: 4,395 + 2,950 VALU per permutation.
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void leaf_hash_list_mix_kernel(
+    const uint8_t *__restrict__ shards, uint32_t S, RowMap rows, size_t inst_stride,
+    const uint2 *__restrict__ list, const uint32_t *__restrict__ counter,
+    uint8_t *__restrict__ nodes, size_t node_inst_stride) {
+    const uint32_t L = *counter;
+    const uint32_t lo = (uint32_t)((uint64_t)blockIdx.x * L / gridDim.x);
+    const uint32_t nb = (uint32_t)((uint64_t)(blockIdx.x + 1) * L / gridDim.x) - lo;
+    const uint32_t rem = nb & 255u;
+    const uint32_t np = rem <= 128u ? rem : 0u;   // pair-lane sponges of this block
+    const uint32_t ns = nb - np;                  // one-lane sponges, in rounds of 256
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t d[8];
+    if (wave < 4) {
+        for (uint32_t t = threadIdx.x; t < ns; t += 256) {
+            const uint2 e = list[lo + t];
+            sha3_256_row(shards + e.x * inst_stride + rows.off(e.y), S, d);
+            store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
+        }
+        return;
+    }
+    const uint32_t q = (np + 3) >> 2;   // sponges per pair-lane wave (<= 32)
+    const uint32_t pi = (threadIdx.x & 63u) >> 1, h = threadIdx.x & 1u;
+    const uint32_t i = (wave - 4) * q + pi;
+    if (pi >= q || i >= np) return;     // both lanes of a pair leave together
+    const uint2 e = list[lo + ns + i];
     sha3_256_row_pl(shards + e.x * inst_stride + rows.off(e.y), S, h, d);
     if (!h) store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
 }
@@ -1304,7 +1486,9 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
                        piece, a.payload, a.payload_stride, a.payload_S, a.payload_k, a.rstatus)
 #define HB_BS_CASE(RT)                                                                           \
     case RT:                                                                                     \
-        if (a.mode == 3)                                                                         \
+        if (a.mode == 4)                                                                         \
+            HB_BS_LAUNCH(RT, 4);                                                                 \
+        else if (a.mode == 3)                                                                    \
             HB_BS_LAUNCH(RT, 3);                                                                 \
         else if (a.mode == 2)                                                                    \
             HB_BS_LAUNCH(RT, 2);                                                                 \
@@ -1401,6 +1585,18 @@ hipError_t launch_leaf_hash_rebuilt(const uint8_t *shards, size_t shard_len, con
         const char *e = getenv("HBRBC_LIST_PAIR_BELOW");
         return e ? (size_t)atoll(e) : ((size_t)1 << 18);
     }();
+    // below it the balanced form (one block per CU, the split decided on the
+    // device from the list length); HBRBC_LIST_FORM=pair: all pair-lane (A/B)
+    static const bool form_pair = [] {
+        const char *e = getenv("HBRBC_LIST_FORM");
+        return e && !strcmp(e, "pair");
+    }();
+    if (total < pair_below && !form_pair) {
+        hipLaunchKernelGGL(leaf_hash_list_mix_kernel, dim3((unsigned)std::max(1, g_num_cus)),
+                           dim3(512), 0, s, shards, (uint32_t)shard_len, rows, inst_stride, list,
+                           counter, nodes, node_inst_stride);
+        return hipGetLastError();
+    }
     if (total < pair_below) {
         hipLaunchKernelGGL(leaf_hash_list_pl_kernel, dim3(grid_for(2 * total, (size_t)1 << 30)),
                            dim3(kBlock), 0, s, shards, (uint32_t)shard_len, rows, inst_stride,
