@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--no-sm-overlap", action="store_true",
                     help="validator mode on one rank: run each step's state machine after its "
                          "decode instead of beside the next step's data plane")
+    ap.add_argument("--vpipes", type=int, default=int(os.environ.get("HBRBC_BENCH_VPIPES", "2")),
+                    help="one rank: step pipelines on their own HIP streams, step i on pipe "
+                         "i %% vpipes (each with its own buffers and state machines)")
     ap.add_argument("--vsubs", type=int, default=4,
                     help="validator mode with >1 rank: pipelined sub-batches per step")
     ap.add_argument("--mode", choices=["instances", "validators", "both"], default="both",
@@ -585,8 +588,9 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     import torch
     import torch.distributed as dist
 
-    from hbbft_amd.sharded import (CommTimer, DistExchange, ShardedBroadcast, SoloExchange,
-                                   overlapped_steps, pipelined_step)
+    from hbbft_amd.sharded import (CommTimer, DistExchange, OverlapPipe, ShardedBroadcast,
+                                   SoloExchange, interleaved_steps, overlapped_steps,
+                                   pipelined_step)
 
     nsub = max(1, min(args.vsubs, count)) if world > 1 else 1
     # one rank: the state machine of step i on a side stream beside the data
@@ -605,6 +609,13 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                             pstride, dev) for i in range(nsub)]
 
     side = torch.cuda.Stream(dev) if overlap else None
+    # one rank, vpipes > 1: whole-step pipelines side by side on their own
+    # streams (each its own ShardedBroadcast: buffers, library context, two
+    # state-machine slots), step i on pipe i % vpipes
+    npipe = max(1, args.vpipes) if overlap else 1
+    pipe_sbs = [sb] + [ShardedBroadcast(n, count, plen, rank, world, device=local, sm_slots=2)
+                       for _ in range(npipe - 1)]
+    pipe_streams = [(torch.cuda.Stream(dev), torch.cuda.Stream(dev)) for _ in range(npipe)]
 
     def step():
         if world > 1:   # sub-batches with every exchange in flight behind compute
@@ -613,16 +624,21 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
             sb.step(pay_sub[0], ex)
 
     def run_steps(k, timing=None):
-        if overlap:
+        if overlap and npipe > 1:
+            pipes = [OverlapPipe(p_, ex, s_[1], main=s_[0], timing=timing)
+                     for p_, s_ in zip(pipe_sbs, pipe_streams)]
+            interleaved_steps(pipes, [pay_sub[0]] * npipe, k)
+        elif overlap:
             overlapped_steps(sb, pay_sub[0], ex, k, side, timing)
         else:
             for _ in range(k):
                 step()
 
-    run_steps(args.warmup)
+    run_steps(max(args.warmup, npipe))   # every pipe has stepped before the check
     torch.cuda.synchronize(dev)
     if not args.no_verify:
-        for i, s_ in enumerate(subs):
+        for i, s_ in enumerate(subs + pipe_sbs[1:]):
+            i = min(i, len(bounds) - 2)
             c = bounds[i + 1] - bounds[i]
             assert bool((s_.ok_v == 1).all()), "a valid Value proof was rejected"
             assert bool((s_.status == 0).all()), "decode failed"
@@ -632,7 +648,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                 exp = gen_payloads(torch, SEED, src * count + bounds[i], c, plen, pstride, dev)
                 assert torch.equal(s_.out[src * c:(src + 1) * c, :plen], exp[:, :plen]), \
                     "decoded payload differs"
-    for s_ in subs:
+    for s_ in subs + pipe_sbs[1:]:
         s_.rb.profile(True)
         s_.rb.profile_reset()
     timer.reset()
@@ -649,7 +665,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    for s_ in subs:
+    for s_ in subs + pipe_sbs[1:]:
         s_.rb.profile(False)
     if overlap:   # spans on the side stream, beside the next step's data plane
         sm_ms = sum(e0.elapsed_time(e1) for e0, e1 in sm_side) / args.steps
@@ -673,10 +689,12 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         per_rank = [mine]
     stages = {}
     counts = {}
-    for s_ in subs:
+    for s_ in subs + pipe_sbs[1:]:
         for st_name, (ms, cnt) in s_.rb.profile_read().items():
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
+        if s_ is not sb and s_ in pipe_sbs:
+            continue   # a step runs on one pipe: its work is one object's
         for key, v in s_.counts().items():
             # sub-batches run their state machines in lockstep: rounds are shared
             counts[key] = max(counts.get(key, 0), v) if key == "state_machine_rounds" \
@@ -706,11 +724,12 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                    "proposals_per_gpu": count, "instances_per_step": count * world,
                    "parallelism": "validator-sharded x%d" % world,
                    "pipelined_sub_batches": nsub,
+                   "step_pipelines": npipe,
                    # per-rank device bytes of this object at 1/2/4/8 GPUs (rank 0;
                    # hbbft_amd.sharded.rank_footprint, torch buffers + reconstruct
                    # workspace bound), against 288 GB of HBM per MI355X
                    "hbm_footprint_per_rank": footprint_summary(n, count, plen,
-                                                               2 if overlap else 1)},
+                                                               2 if overlap else 1, npipe)},
         "exchange": {"ms_per_step": xms, "bytes_per_step_per_gpu": xbytes,
                      "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
                      "backend": ex.backend, "per_rank": per_rank},
@@ -718,20 +737,28 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         "stages_ms_per_step": dict({s: stages[s][0] / args.steps for s in stages},
                                    **({"state_machine_overlapped": sm_ms} if overlap
                                       else {"state_machine": sm_ms})),
+        **({"stages_note": "%d step pipelines run side by side: a stage's span includes the "
+                           "other pipelines' kernels (--vpipes 1 gives the serial split)" % npipe}
+           if npipe > 1 else {}),
         "state_machine_schedule": ("step i's rounds on a second HIP stream beside step i + 1's "
                                    "data plane (two state-machine slots); every step's rounds "
                                    "complete inside the timed region" if overlap else
-                                   "after each step's decode, in lockstep over the ranks"),
+                                   "after each step's decode, in lockstep over the ranks")
+                                  + ("; %d step pipelines side by side on their own streams, "
+                                     "step i on pipe i %% %d (stage times overlap)" % (npipe, npipe)
+                                     if npipe > 1 else ""),
     }
 
 
-def footprint_summary(n, count, plen, sm_slots=1):
+def footprint_summary(n, count, plen, sm_slots=1, pipes=1):
     from hbbft_amd.sharded import HBM_PER_GPU, rank_footprint
     out = {}
     for g in (1, 2, 4, 8):
-        # (two state-machine slots only where they are used: one rank)
+        # (two state-machine slots and the step pipelines only where they are
+        # used: one rank)
         fp = rank_footprint(n, count, plen, g, 0, sm_slots=sm_slots if g == 1 else 1)
-        out["G%d" % g] = {"bytes": fp["total_bytes"], "frac_of_288GB": fp["frac_of_hbm"],
+        k = pipes if g == 1 else 1
+        out["G%d" % g] = {"bytes": k * fp["total_bytes"], "frac_of_288GB": k * fp["frac_of_hbm"],
                           "echo_slab_bytes": fp["buffers"].get("echo_sh", fp["buffers"]["slab"])}
     assert all(v["bytes"] < HBM_PER_GPU for v in out.values()), out
     return out

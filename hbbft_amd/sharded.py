@@ -638,64 +638,106 @@ def pipelined_step(subs, payloads, ex, timer):
         sb.sm_rounds = rounds
 
 
-def overlapped_steps(sb, payloads, ex, steps, side, timing=None):
-    """`steps` steps of one rank with no process group (world 1), the state
+class OverlapPipe:
+    """The steps of one rank with no process group (world 1), the state
     machine of step i on the `side` stream beside the data plane of step
-    i + 1 on the current stream (sb built with sm_slots=2; the slots
+    i + 1 on the `main` stream (sb built with sm_slots=2; the slots
     alternate).  The rounds are latency-bound at low occupancy, the data
     plane's sponges issue-bound: side by side the GPU fills the one's idle
     issue slots with the other's work.  Step i's rounds start after step
     i + 1's encoder: the LDS-staged encoder needs 48 KB of LDS per workgroup
     and ran at half speed beside the rounds' LDS images (validator cfg4:
-    encode 0.69 -> 1.50 ms), the sponge kernels use none.  Every step's
-    rounds have completed (and sb.decided holds the last step's flags) when
-    this returns; `timing`: a list that receives (start, end) events of each
-    step's rounds on the side stream."""
-    from .rbc_sim import LocalRounds
-    assert len(sb.sms) == 2 and ex.world == 1
-    cur = torch.cuda.current_stream()
+    encode 0.69 -> 1.50 ms), the sponge kernels use none.  `timing`: a list
+    that receives (start, end) events of each step's rounds on the side
+    stream."""
 
-    def launch(slot, ready, after):
+    def __init__(self, sb, ex, side, main=None, timing=None):
+        assert len(sb.sms) == 2 and ex.world == 1
+        self.sb, self.ex, self.side = sb, ex, side
+        self.main = main if main is not None else torch.cuda.current_stream()
+        # the buffers and payloads were written on the caller's stream
+        self.main.wait_stream(torch.cuda.current_stream())
+        side.wait_stream(torch.cuda.current_stream())
+        self.timing = timing
+        self.steps = 0
+        self.prev_ready = None   # step i - 1's data plane is done (its outcomes are in)
+
+    def _launch(self, slot, ready, after):
+        from .rbc_sim import LocalRounds
+        side = self.side
         side.wait_event(ready)
         if after is not None:
             side.wait_event(after)
         ev = None
-        if timing is not None:
+        if self.timing is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(side)
-            timing.append(ev)
-        return slot, LocalRounds([sb.sms[slot]], loopback=False, stream=side).launch(), ev
+            self.timing.append(ev)
+        return slot, LocalRounds([self.sb.sms[slot]], loopback=False, stream=side).launch(), ev
 
-    def drain(p):
+    def _drain(self, p):
         slot, lr, ev = p
+        sb = self.sb
         rounds = lr.wait()
         prev = sb.slot
         sb.slot = slot
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(self.side):
             sb.finish()
             if ev is not None:
                 ev[1].record()
         sb.slot = prev
         sb.sm_rounds = rounds
 
-    prev_ready = None   # step i - 1's data plane is done (its outcomes are in)
-    for i in range(steps):
-        sb.slot = i % 2
-        sb.encode_phase(payloads)
-        after_encode = torch.cuda.Event()
-        after_encode.record(cur)
-        running = None
-        if prev_ready is not None:   # step i - 1's rounds, after step i's encoder
-            running = launch((i - 1) % 2, prev_ready, after_encode)
-        sb.rest_phase(ex)
-        prev_ready = torch.cuda.Event()
-        prev_ready.record(cur)
+    def step(self, payloads):
+        """Enqueue one step; returns after the previous step's rounds."""
+        sb, i = self.sb, self.steps
+        with torch.cuda.stream(self.main):
+            sb.slot = i % 2
+            sb.encode_phase(payloads)
+            after_encode = torch.cuda.Event()
+            after_encode.record(self.main)
+            running = None
+            if self.prev_ready is not None:   # step i - 1's rounds, after step i's encoder
+                running = self._launch((i - 1) % 2, self.prev_ready, after_encode)
+            sb.rest_phase(self.ex)
+            self.prev_ready = torch.cuda.Event()
+            self.prev_ready.record(self.main)
         if running is not None:
-            drain(running)           # host read; step i's data plane is queued
-    if prev_ready is not None:
-        drain(launch((steps - 1) % 2, prev_ready, None))
-    sb.slot = (steps - 1) % 2
-    cur.wait_stream(side)
+            self._drain(running)              # host read; step i's data plane is queued
+        self.steps += 1
+
+    def finish(self):
+        """Run the last step's rounds; every step's rounds have completed (and
+        sb.decided holds the last step's flags) when this returns, and the
+        caller's current stream waits for both streams."""
+        if self.prev_ready is not None:
+            self._drain(self._launch((self.steps - 1) % 2, self.prev_ready, None))
+            self.prev_ready = None
+        self.sb.slot = (self.steps - 1) % 2
+        cur = torch.cuda.current_stream()
+        cur.wait_stream(self.main)
+        cur.wait_stream(self.side)
+
+
+def overlapped_steps(sb, payloads, ex, steps, side, timing=None):
+    """`steps` steps of one OverlapPipe on the current stream."""
+    pipe = OverlapPipe(sb, ex, side, timing=timing)
+    for _ in range(steps):
+        pipe.step(payloads)
+    pipe.finish()
+
+
+def interleaved_steps(pipes, payloads, steps):
+    """`steps` steps over several OverlapPipes on their own streams (world 1),
+    step i on pipes[i % len(pipes)]: the pipes' data planes run side by side,
+    so a sponge launch of one (4,096 lockstep waves at validator cfg3, one
+    residency round) shares the SIMDs with another pipe's kernels instead of
+    running in one synchronous round, and one pipe's rebuilt-row list and
+    state machine leave their idle issue slots to the other."""
+    for i in range(steps):
+        pipes[i % len(pipes)].step(payloads[i % len(pipes)])
+    for p in pipes:
+        p.finish()
 
 
 def run_state_machines(subs, ex):

@@ -272,6 +272,34 @@ def test_sharded_single_rank_step():
     assert np.array_equal(sb.out.cpu().numpy()[:, :plen], pay)
 
 
+@pytest.mark.gpu
+def test_sharded_overlapped_and_interleaved_steps():
+    """The one-rank schedules the bench runs: each step's state machine on a
+    side stream beside the next step's data plane (two state-machine slots),
+    and two such step pipelines side by side on their own streams.  Every
+    object decodes its own payloads and every instance is decided."""
+    from hbbft_amd.sharded import OverlapPipe, interleaved_steps, overlapped_steps
+    n, count, plen = 64, 4, 11916 * 22 - 4
+    sb = ShardedBroadcast(n, count, plen, 0, 1, device=0, sm_slots=2)
+    pay, t = _payloads(21, count, plen, sb.device)
+    timing = []
+    overlapped_steps(sb, t, SoloExchange(), 3, torch.cuda.Stream(sb.device), timing)
+    torch.cuda.synchronize()
+    assert len(timing) == 3 and sb.sm_rounds > 0
+    assert (sb.status.cpu().numpy() == 0).all() and sb.decided.cpu().all()
+    assert np.array_equal(sb.out.cpu().numpy()[:, :plen], pay)
+    objs = [ShardedBroadcast(n, count, plen, 0, 1, device=0, sm_slots=2) for _ in range(2)]
+    pays = [_payloads(40 + i, count, plen, objs[i].device) for i in range(2)]
+    pipes = [OverlapPipe(o, SoloExchange(), torch.cuda.Stream(o.device), main=torch.cuda.Stream(o.device))
+             for o in objs]
+    interleaved_steps(pipes, [p[1] for p in pays], 5)   # pipe 0: steps 0, 2, 4; pipe 1: 1, 3
+    torch.cuda.synchronize()
+    assert [p.steps for p in pipes] == [3, 2]
+    for o, (p, _) in zip(objs, pays):
+        assert (o.status.cpu().numpy() == 0).all() and o.decided.cpu().all()
+        assert np.array_equal(o.out.cpu().numpy()[:, :plen], p)
+
+
 def _gloo_gpu_worker(rank, world, port, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
