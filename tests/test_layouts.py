@@ -299,3 +299,41 @@ def test_validate_rows_subset_with_indices(torch_cuda):
             assert np.array_equal(lv[:, j], nd[:, j])
         else:
             assert not lv[:, j].any()
+
+
+@pytest.mark.parametrize("count,n_erase", [(2, 21), (1500, 42), (3000, 30), (3000, 42), (6000, 42)])
+def test_rebuilt_row_list_lengths(torch_cuda, count, n_erase):
+    """A decode with known leaves re-hashes only the rebuilt rows, through
+    the balanced list kernel (leaf_hash_list_mix_kernel, kernels.hip) below
+    2^18 listed rows of the worst case.  The list lengths here take each of its
+    branches per CU share: pair-lane only (<= 128), one-lane only (129..256),
+    one round plus a pair-lane remainder, two and four one-lane rounds.  The
+    decode tree must come out as the proposer's tree."""
+    torch = torch_cuda
+    n, f, plen = 64, 21, 2000
+    rb = hb.RbcBatch(n, f, device=0)
+    S = hb.shard_len(plen, rb.k)
+    pay, p = payloads(torch, 77, count, plen)
+    slab = rb.alloc_slab(count, S)
+    nodes = rb.alloc_nodes(count)
+    rb.frame_encode(p, plen, slab)
+    rb.merkle(slab, S, nodes)
+    rng = np.random.default_rng(count + n_erase)
+    pres = np.ones((count, n), np.uint8)
+    np.put_along_axis(pres, np.argsort(rng.random((count, n)), axis=1)[:, :n_erase], 0, axis=1)
+    pres_d = torch.from_numpy(pres).cuda()
+    keep = pres_d.bool()
+    rec = slab.clone()
+    rec[~keep] = 0xA5                              # garbage in the erased rows
+    nodes2 = rb.alloc_nodes(count)
+    nodes2.fill_(0x33)
+    nodes2[:, :n] = torch.where(keep[:, :, None], nodes[:, :n], nodes2[:, :n])
+    ostride = max(16, (rb.k * S + 15) // 16 * 16)
+    out = torch.zeros((count, ostride), dtype=torch.uint8, device="cuda")
+    plo = torch.zeros(count, dtype=torch.int32, device="cuda")
+    status = torch.ones(count, dtype=torch.int32, device="cuda")
+    rb.decode(rec, S, pres_d, nodes[:, -1, :].clone(), nodes2, out, plo, status, known_leaves=True)
+    torch.cuda.synchronize()
+    assert (status == 0).all() and (plo == plen).all()
+    assert torch.equal(rec, slab) and torch.equal(nodes2, nodes)
+    assert torch.equal(out[:, :plen].cpu(), torch.from_numpy(pay))
