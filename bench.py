@@ -45,7 +45,10 @@ SEED = 0x48424246              # "HBBF"
 CONFIGS = {
     # name: (N, payload bytes, instances per GPU, erasures, validator-mode proposals per GPU)
     "cfg2": (16, 1 << 20, 4096, "f", 512),
-    "cfg3": (64, 256 << 10, 16384, "f", 4096),
+    # cfg3: 32768 instances = 8 residency rounds of 4 waves/SIMD per sponge launch
+    # (16384: 4 rounds, ~2 % slower per instance -- ramp and tail,
+    # profiles/r4y_count_ab.txt, r4t_sponge_residency.txt)
+    "cfg3": (64, 256 << 10, 32768, "f", 4096),
     "cfg4": (128, 256 << 10, 8192, "f", 2048),
     "cfg5": (250, 4 << 20, 1024, "worst", 128),
 }
