@@ -48,8 +48,10 @@ CONFIGS = {
     # cfg3: 32768 instances = 8 residency rounds of 4 waves/SIMD per sponge launch
     # (16384: 4 rounds, ~2 % slower per instance -- ramp and tail,
     # profiles/r4y_count_ab.txt, r4t_sponge_residency.txt)
-    "cfg3": (64, 256 << 10, 32768, "f", 4096),
-    "cfg4": (128, 256 << 10, 8192, "f", 2048),
+    # validator objects: 8192 / 4096 proposals per GPU (+2.6 / +2.8 % over 4096 / 2048
+    # on one GPU, profiles/r4aa_vcount_ab.txt; G=8 footprint 0.3 of HBM, tests/test_sharded.py)
+    "cfg3": (64, 256 << 10, 32768, "f", 8192),
+    "cfg4": (128, 256 << 10, 8192, "f", 4096),
     "cfg5": (250, 4 << 20, 1024, "worst", 128),
 }
 METRIC = "RBC encode+Merkle+decode payload GB/s, N=64, 1/8 GPUs; fraction of HBM peak"

@@ -351,7 +351,7 @@ def test_sharded_two_ranks_gloo_on_one_gpu():
 
 
 # ----------------------------------------------------------- HBM footprint --
-BENCH_OBJECTS = [("cfg3", 64, 256 << 10, 4096), ("cfg4", 128, 256 << 10, 2048)]
+BENCH_OBJECTS = [("cfg3", 64, 256 << 10, 8192), ("cfg4", 128, 256 << 10, 4096)]
 
 
 @pytest.mark.parametrize("cfg,n,plen,count", BENCH_OBJECTS)
