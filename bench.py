@@ -51,8 +51,10 @@ CONFIGS = {
     # validator objects: 8192 / 4096 proposals per GPU (+2.6 / +2.8 % over 4096 / 2048
     # on one GPU, profiles/r4aa_vcount_ab.txt; G=8 footprint 0.3 of HBM, tests/test_sharded.py)
     "cfg3": (64, 256 << 10, 32768, "f", 8192),
-    "cfg4": (128, 256 << 10, 8192, "f", 4096),
-    "cfg5": (250, 4 << 20, 1024, "worst", 128),
+    "cfg4": (128, 256 << 10, 16384, "f", 4096),
+    # cfg2 keeps BASELINE's batch of 4096; cfg4 / cfg5 name none: 16384 / 2048
+    # instances (+1 / +5 % over 8192 / 1024, profiles/r4ac_count_ab.txt)
+    "cfg5": (250, 4 << 20, 2048, "worst", 128),
 }
 METRIC = "RBC encode+Merkle+decode payload GB/s, N=64, 1/8 GPUs; fraction of HBM peak"
 
