@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 import torch
 
 import bench
@@ -50,3 +51,28 @@ def test_f4_leg_host_helpers():
     assert bench.f4_cpu_check(pool[0]) and bench.f4_cpu_check(pool[3])
     ops, src = bench.pairing_ops_per_check()
     assert ops is not None and 1e6 < ops < 1e8 and "SQ_INSTS_VALU" in src
+
+
+@pytest.mark.gpu
+def test_bench_line_small():
+    """The whole default line at small sizes on the GPU, as the driver runs it
+    (one process, N=1): instance mode with its leaf-reuse variant, both
+    validator objects on the one-rank schedule (state machine beside the next
+    step, two step pipelines), the f4 leg.  bench.py checks every decoded
+    payload itself after the warm-up; here the line must carry every object,
+    none of them an error."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--count", "512",
+                        "--vcount", "256", "--steps", "2", "--warmup", "2", "--no-cpu",
+                        "--f4-checks", "4096", "--f4-steps", "1"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["value"] > 0 and line["n_gpus"] == 1 and line["config"]["instances_per_gpu"] == 512
+    assert line["leaf_reuse"]["value"] > 0
+    for key in ("validators", "validators_cfg4"):
+        v = line[key]
+        assert "error" not in v, v.get("error")
+        assert v["value"] > 0 and v["config"]["step_pipelines"] == 2
+        assert "state_machine_overlapped" in v["stages_ms_per_step"]
+    assert "error" not in line["threshold_decrypt"]
