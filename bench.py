@@ -41,6 +41,7 @@ KECCAK_OPS_PER_PERM = 4320     # static count: 180 VALU per round x 24 rounds (D
 # 4 waves/SIMD, profiles/r1_valu_microbench.txt): v_alignbit issues at half rate
 KECCAK_CEILING_PERMS = 10.48e9
 SEED = 0x48424246              # "HBBF"
+GARBAGE64 = -0x5A5A5A5A5A5A5A5B  # 0xA5A5A5A5A5A5A5A5 as int64: the erase stage's fill
 
 CONFIGS = {
     # name: (N, payload bytes, instances per GPU, erasures, validator-mode proposals per GPU)
@@ -77,6 +78,10 @@ def parse():
     ap.add_argument("--f4-steps", type=int, default=3)
     ap.add_argument("--no-cfg4", action="store_true",
                     help="skip the cfg4 validator-sharded object of the default cfg3 line")
+    ap.add_argument("--no-riders", action="store_true",
+                    help="skip the cfg2 / cfg5 instance-mode objects of the default cfg3 line")
+    ap.add_argument("--rider-count", type=int, default=0,
+                    help="instances per GPU of the cfg2 / cfg5 objects (default: their config)")
     ap.add_argument("--streams", type=int, default=1,
                     help="instance mode: sub-batches per step, each on its own HIP stream")
     ap.add_argument("--stagger", action="store_true",
@@ -256,14 +261,14 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
                   "ops_per_perm": opp, "ops_per_perm_source": src,
                   "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
                   "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS,
-                  "profiled": profiled_frac(config, perms[dom], opp)})
+                  "profiled": profiled_frac(config, perms[dom], opp, per_launch)})
     else:
         r.update({"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": hbm_gbs / HBM_PEAK_GBS})
     return r
 
 
-def profiled_frac(config, perms_per_launch, opp):
+def profiled_frac(config, perms_per_launch, opp, per_launch):
     """The same roofline from committed files only: the dominant kernel's
     average duration in the rocprofv3 --kernel-trace --stats summary named by
     profiles/roofline_sources.json[config], and the SQ_INSTS_VALU counter of
@@ -280,14 +285,17 @@ def profiled_frac(config, perms_per_launch, opp):
                 break
         if avg_ns is None:
             return None
+        if int(src["instances"]) != int(per_launch):
+            # a different batch per launch (--count / --streams): the committed
+            # profile is not this line's configuration
+            return None
     except (OSError, ValueError, KeyError):
         return None
     pps = perms_per_launch / (avg_ns * 1e-9)
     return {"kernel_stats": src["kernel_stats"], "kernel": src["kernel"],
             "avg_ms": avg_ns / 1e6, "perms_per_s": pps, "ops_per_perm": opp,
             "lane_ops_per_s": pps * opp, "frac": pps * opp / VALU_PEAK_OPS,
-            "note": "valid when this line's instances per launch equal the profiled run's (%s)"
-                    % src.get("instances", "?")}
+            "instances_per_launch": src["instances"]}
 
 
 def valu_ops_per_perm(config):
@@ -353,12 +361,18 @@ def cpu_baseline(args, n, f, plen, n_erase, config):
 
 
 # -------------------------------------------------------------- instance mode --
-def run_instances(args, n, plen, count, erase, rank, world, dev, local):
+def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=None,
+                  streams=None, leaf_reuse=True, encode_merkle=False):
+    """One instance-mode object: `config` labels it (default --config); the
+    headline passes streams / leaf_reuse from the command line, the riders
+    (cfg2, cfg5) run one stream without the leaf-reuse variant, and cfg2 adds
+    BASELINE's encode+Merkle rate (`encode_merkle`)."""
     import torch
     import torch.distributed as dist
 
     import hbbft_amd as hb
-    nsub = max(1, min(args.streams, count))
+    config = config or args.config
+    nsub = max(1, min(args.streams if streams is None else streams, count))
     f = (n - 1) // 3
     subs_rb = [hb.RbcBatch(n, f, device=local) for _ in range(nsub)]
     rb = subs_rb[0]
@@ -396,7 +410,27 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
     plen_out = torch.empty(count, dtype=torch.int32, device=dev)
     status = torch.empty(count, dtype=torch.int32, device=dev)
 
+    # Transport: the receiver never holds the rows its pattern erases.  Every
+    # step overwrites them with garbage (the "erase" stage: one row fill,
+    # f x stride bytes per instance) after validation and before the decode,
+    # so every timed decode really rebuilds them and the fused unframe really
+    # writes the payload from rebuilt rows (the decode never runs on rows
+    # that still hold the right bytes).  The row ids of every pattern (and
+    # sub-batch) are built here, outside the timed region.
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
+    erase_spans = []
+
+    def erase_rows(i, q):
+        sl = slice(bounds[q], bounds[q + 1])
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        subs_rb[q].drop_rows(slab[sl], pool[i % len(pool)][sl], 0xA5)   # hbrbc_drop_rows
+        e1.record()
+        if timing_erase[0]:
+            erase_spans.append((e0, e1))
+    timing_erase = [False]
+
     main = torch.cuda.current_stream(dev)
     subs = []
     for i in range(nsub):
@@ -405,7 +439,7 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
         sb.reserve(hi - lo)
         subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
 
-    def run_sub(sb, sl, pres, after_encode=None):
+    def run_sub(sb, sl, pres, i, q, after_encode=None):
         sb.frame_encode(payloads[sl], plen, slab[sl])   # frame folded into the encoder
         if after_encode is not None:
             after_encode()
@@ -413,58 +447,56 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
         sb.proofs(nodes[sl], digests[sl], ndig[sl])
         sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
         roots[sl].copy_(nodes[sl, -1, :])      # what the Echo/Ready quorum agreed on
+        erase_rows(i, q)
         sb.decode(slab[sl], S, pres[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
                   status[sl])
 
     def step(i):
         pres = pool[i % len(pool)]
         if nsub == 1:
-            run_sub(subs[0][0], subs[0][2], pres)
+            run_sub(subs[0][0], subs[0][2], pres, i, 0)
             return
         ev = torch.cuda.Event()
         ev.record(main)
         prev = ev
-        for sb, st, sl in subs:
+        for q, (sb, st, sl) in enumerate(subs):
             st.wait_event(prev)
             with torch.cuda.stream(st):
                 if args.stagger:
                     # the next sub-batch starts when this one's encode is done:
                     # its encode (HBM-heavy) runs beside this one's sponges
                     nxt = torch.cuda.Event()
-                    run_sub(sb, sl, pres, after_encode=lambda: nxt.record(st))
+                    run_sub(sb, sl, pres, i, q, after_encode=lambda: nxt.record(st))
                     prev = nxt
                 else:
-                    run_sub(sb, sl, pres)
+                    run_sub(sb, sl, pres, i, q)
         for _, st, _ in subs:
             main.wait_stream(st)
+
+    def check(what):
+        """Every proof valid, every decode Ok, every payload byte, and the
+        decode trees equal to the proposer's -- the rebuilt rows hash to the
+        same leaves, so every rebuilt byte is right."""
+        assert bool((ok == 1).all()), "%s: a valid proof was rejected" % what
+        assert bool((status == 0).all()), "%s: decode failed" % what
+        assert bool((plen_out == plen).all()), what
+        assert torch.equal(out[:, :plen], payloads[:, :plen]), "%s: decoded payload differs" % what
+        assert torch.equal(nodes2, nodes), "%s: rebuilt rows differ" % what
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
     if not args.no_verify:
-        assert bool((ok == 1).all()), "a valid proof was rejected"
-        assert bool((status == 0).all()), "decode failed"
-        assert bool((plen_out == plen).all())
-        assert torch.equal(out[:, :plen], payloads[:, :plen]), "decoded payload differs"
-        # decode once more from a copy whose erased rows hold garbage: the
-        # timed steps decode in place, where erased rows still hold the right
-        # bytes, so only this pass shows the rebuild itself is correct
-        present = pool[(args.warmup - 1) % len(pool)]
-        vs = slab.clone()
-        vs[present == 0] = 0xA5
-        out.zero_()
-        for sb, _, sl in subs:
-            sb.decode(vs[sl], S, present[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
-                      status[sl])
-        torch.cuda.synchronize(dev)
-        assert bool((status == 0).all()), "decode from garbage-filled erasures failed"
-        assert torch.equal(out[:, :plen], payloads[:, :plen]), "rebuilt payload differs"
-        assert torch.equal(vs, slab) and torch.equal(nodes2, nodes), "rebuilt rows differ"
-        del vs
+        check("warm-up")
+        # the last warm-up step's erased rows were garbage before its decode:
+        # poison the payload buffer too, so the timed steps' outputs are theirs
+        out.fill_(0x5A)
+        nodes2.fill_(0x5A)
 
     for sb in subs_rb:
         sb.profile(True)
         sb.profile_reset()
+    timing_erase[0] = True
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -475,47 +507,76 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    timing_erase[0] = False
     for sb in subs_rb:
         sb.profile(False)
     elapsed = max_over_ranks(elapsed, world, dev)
+    verified = False
+    if not args.no_verify:
+        check("last timed step")   # the outputs of the last timed step, from garbage rows
+        verified = True
     stages = {}
     for sb in subs_rb:
         for st_name, (ms, cnt) in sb.profile_read().items():
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
+    stages["erase"] = (sum(a.elapsed_time(b) for a, b in erase_spans), len(erase_spans))
     value = float(count) * plen * world * args.steps / elapsed / 1e9
     lr = None
-    if not args.no_leaf_reuse and nsub == 1 and erase == "f":
+    if leaf_reuse and not args.no_leaf_reuse and nsub == 1 and erase == "f":
         lr = run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests,
-                            ndig, ok, out, plen_out, status, S, n, f, world, dev)
+                            ndig, ok, out, plen_out, status, S, n, f, world, dev,
+                            erase_rows)
+    em = None
+    if encode_merkle:
+        em = run_encode_merkle(args, rb, payloads, plen, slab, nodes, digests, ndig, S, world,
+                               dev, count)
     roof = roofline_of(stages, args.steps, count / nsub, n, k, m, S, plen, rb.node_count,
-                       rb.dslots, n_erase, elapsed, args.config,
+                       rb.dslots, n_erase, elapsed, config,
                        unframe_fused=rb.unframe_fused(S, out.stride(0)))
     roof["unframe_fused"] = rb.unframe_fused(S, out.stride(0))
-    return {
-        "value": value, "ms_per_step": elapsed / args.steps * 1e3, "roofline": roof,
+    r = {
+        "value": value, "unit": "GB/s", "ms_per_step": elapsed / args.steps * 1e3,
+        "roofline": roof,
         "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
         "config": {"workload": "%s: N=%d f=%d (%d+%d shards), %d B payloads, %d instances/GPU, "
-                               "%s erasures" % (args.config, n, f, k, m, plen, count,
+                               "%s erasures" % (config, n, f, k, m, plen, count,
                                                 "f random" if erase == "f" else "worst-case"),
                    "n": n, "f": f, "payload_bytes": plen, "shard_len": S,
                    "instances_per_gpu": count, "global_batch": count * world,
                    "parallelism": "instance-sharded x%d" % world, "streams_per_gpu": nsub},
         "n_erase": n_erase, "f": f, "leaf_reuse": lr,
+        "verified_last_timed_step": verified,
+        "decode_input": ("every step overwrites the %d erased rows of each instance with garbage "
+                         "after validation (stage `erase`), so each timed decode rebuilds them; "
+                         "the last timed step's payloads and decode trees are checked"
+                         % n_erase),
     }
+    if em is not None:
+        r["encode_merkle"] = em
+    return r
 
 
 def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests, ndig,
-                   ok, out, plen_out, status, S, n, f, world, dev):
+                   ok, out, plen_out, status, S, n, f, world, dev, erase_rows):
     """Labelled variant of the instance step, NOT the headline: validate
     writes each validated row's Merkle leaf into the decode tree
     (hbrbc_validate_rows leaf_out), and the decode hashes only the rows the
     reconstruct rebuilds (known_leaves).  A node can do exactly this with
     the Echoes it validated (broadcast.rs:291 validate_proof, then 580
     MerkleTree::from_vec over the same rows); the reference hashes them
-    again.  Same inputs, same erasure patterns, same outputs."""
+    again.  Same inputs, same erasure patterns, same outputs; like the
+    headline, every step's erased rows are garbage before its decode, and so
+    are their leaves (the receiver never validated those Echoes)."""
     import torch
     count = slab.shape[0]
+    nc = nodes2.shape[1]
+    leaf_words = nodes2.view(torch.int64).view(count * nc, 4)
+    # leaf slot of erased row (i, j) = i * nc + j (built outside the timed region)
+    leaf_ids = []
+    for p_ in pool:
+        e = torch.nonzero(p_.view(-1) == 0).view(-1)
+        leaf_ids.append((e // n) * nc + e % n)
 
     def step(i):
         pres = pool[i % len(pool)]
@@ -524,30 +585,22 @@ def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, d
         rb.proofs(nodes, digests, ndig)
         rb.validate(slab, S, digests, ndig, nodes, ok, leaf_out=nodes2)
         roots.copy_(nodes[:, -1, :])
+        erase_rows(i, 0)
+        leaf_words.index_fill_(0, leaf_ids[i % len(pool)], GARBAGE64)
         rb.decode(slab, S, pres, roots, nodes2, out, plen_out, status, known_leaves=True)
+
+    def check(what):
+        assert bool((ok == 1).all()) and bool((status == 0).all()), what
+        assert torch.equal(out[:, :plen], payloads[:, :plen]), "leaf reuse %s: payload differs" % what
+        assert torch.equal(nodes2, nodes), "leaf reuse %s: rows/tree differ" % what
 
     for i in range(max(1, args.warmup)):
         step(i)
     torch.cuda.synchronize(dev)
     verified = False
     if not args.no_verify:
-        assert bool((ok == 1).all()) and bool((status == 0).all())
-        assert torch.equal(out[:, :plen], payloads[:, :plen]), "leaf reuse: payload differs"
-        # garbage in the erased rows AND in their leaves: the decode must
-        # rebuild both (the present rows' leaves come from validate)
-        present = pool[(max(1, args.warmup) - 1) % len(pool)]
-        rb.validate(slab, S, digests, ndig, nodes, ok, leaf_out=nodes2)
-        vs = slab.clone()
-        vs[present == 0] = 0xA5
-        nodes2[:, :n][present == 0] = 0x5A
-        out.zero_()
-        rb.decode(vs, S, present, roots, nodes2, out, plen_out, status, known_leaves=True)
-        torch.cuda.synchronize(dev)
-        assert bool((status == 0).all()), "leaf reuse: decode from garbage failed"
-        assert torch.equal(out[:, :plen], payloads[:, :plen]), "leaf reuse: rebuilt payload differs"
-        assert torch.equal(vs, slab) and torch.equal(nodes2, nodes), "leaf reuse: rows/tree differ"
-        del vs
-        verified = True
+        check("warm-up")
+        out.fill_(0x5A)
     rb.profile(True)
     rb.profile_reset()
     if world > 1:
@@ -562,6 +615,9 @@ def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, d
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     rb.profile(False)
+    if not args.no_verify:
+        check("last timed step")
+        verified = True
     stages = {k_: v_[0] / args.steps for k_, v_ in rb.profile_read().items()}
     bl = (S + 1 + 135) // 136          # Keccak blocks per leaf (SHA3-256 rate 136)
     depth = max(1, (n - 1).bit_length())
@@ -570,10 +626,52 @@ def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, d
     executed = tree + n * (bl + depth) + f * bl + (n - 1)
     return {"value": float(count) * plen * world * args.steps / elapsed / 1e9, "unit": "GB/s",
             "ms_per_step": elapsed / args.steps * 1e3, "stages_ms_per_step": stages,
-            "verified_garbage_fill": verified,
+            "verified_last_timed_step": verified,
             "keccak_perms_per_instance": {"faithful": faithful, "executed": executed},
             "note": "labelled variant, not the headline: validate emits the Merkle leaf of each "
-                    "validated row and the decode re-hashes only the f rebuilt rows"}
+                    "validated row and the decode re-hashes only the f rebuilt rows (erased rows "
+                    "and their leaves are garbage before every decode)"}
+
+
+def run_encode_merkle(args, rb, payloads, plen, slab, nodes, digests, ndig, S, world, dev, count):
+    """BASELINE cfg2's own metric: encode + Merkle only -- the proposer half
+    of send_shards (broadcast.rs:170-225: frame, Coding::encode,
+    MerkleTree::from_vec, one proof per shard) over the same batch, timed
+    like the headline; the tree and proofs are checked against the full
+    step's (which validated every proof)."""
+    import torch
+    ref = nodes.clone()
+
+    def step():
+        rb.frame_encode(payloads, plen, slab)
+        rb.merkle(slab, S, nodes)
+        rb.proofs(nodes, digests, ndig)
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize(dev)
+    if not args.no_verify:
+        assert torch.equal(nodes, ref), "encode+Merkle: trees differ"
+    rb.profile(True)
+    rb.profile_reset()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    rb.profile(False)
+    stages = {k_: v_[0] / args.steps for k_, v_ in rb.profile_read().items() if v_[1]}
+    if not args.no_verify:
+        assert torch.equal(nodes, ref), "encode+Merkle: trees differ after the timed steps"
+    del ref
+    return {"metric": "RBC encode+Merkle payload GB/s (frame, encode, tree, N proofs)",
+            "value": float(count) * plen * world * args.steps / elapsed / 1e9, "unit": "GB/s",
+            "ms_per_step": elapsed / args.steps * 1e3, "stages_ms_per_step": stages}
 
 
 def max_over_ranks(x, world, dev):
@@ -599,16 +697,19 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                                    SoloExchange, interleaved_steps, overlapped_steps,
                                    pipelined_step)
 
-    nsub = max(1, min(args.vsubs, count)) if world > 1 else 1
-    # one rank: the state machine of step i on a side stream beside the data
-    # plane of step i + 1 (two state-machine slots)
-    overlap = world == 1 and not args.no_sm_overlap
+    # the state machine of step i on a side stream beside the data plane of
+    # step i + 1 (two state-machine slots), at every world size; at world > 1
+    # its per-round all-gathers run over a process group of their own
+    overlap = not args.no_sm_overlap
+    # serial schedule at world > 1: sub-batches with every exchange in flight
+    nsub = max(1, min(args.vsubs, count)) if world > 1 and not overlap else 1
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
     subs = [ShardedBroadcast(n, bounds[i + 1] - bounds[i], plen, rank, world, device=local,
                              sm_slots=2 if overlap else 1)
             for i in range(nsub)]
     sb = subs[0]
     ex = DistExchange() if world > 1 else SoloExchange()
+    sm_ex = sm_exchange() if world > 1 and overlap else None
     timer = CommTimer(dev)
     pstride = (plen + 15) // 16 * 16 + int(os.environ.get("HBRBC_BENCH_PPAD", "0"))
     # instance (rank s, local i) is global instance s * count + i
@@ -616,9 +717,10 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                             pstride, dev) for i in range(nsub)]
 
     side = torch.cuda.Stream(dev) if overlap else None
-    # one rank, vpipes > 1: whole-step pipelines side by side on their own
-    # streams (each its own ShardedBroadcast: buffers, library context, two
-    # state-machine slots), step i on pipe i % vpipes
+    # vpipes > 1: whole-step pipelines side by side on their own streams (each
+    # its own ShardedBroadcast: buffers, library context, two state-machine
+    # slots), step i on pipe i % vpipes; at world > 1 one pipe's exchanges
+    # overlap the other's compute (what the serial schedule's sub-batches do)
     npipe = max(1, args.vpipes) if overlap else 1
     pipe_sbs = [sb] + [ShardedBroadcast(n, count, plen, rank, world, device=local, sm_slots=2)
                        for _ in range(npipe - 1)]
@@ -630,13 +732,20 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         else:
             sb.step(pay_sub[0], ex)
 
+    xspans = [] if world > 1 else None
+
     def run_steps(k, timing=None):
         if overlap and npipe > 1:
-            pipes = [OverlapPipe(p_, ex, s_[1], main=s_[0], timing=timing)
+            pipes = [OverlapPipe(p_, ex, s_[1], main=s_[0], timing=timing, sm_ex=sm_ex,
+                                 xspans=xspans if timing is not None else None)
                      for p_, s_ in zip(pipe_sbs, pipe_streams)]
             interleaved_steps(pipes, [pay_sub[0]] * npipe, k)
         elif overlap:
-            overlapped_steps(sb, pay_sub[0], ex, k, side, timing)
+            pipe = OverlapPipe(sb, ex, side, timing=timing, sm_ex=sm_ex,
+                               xspans=xspans if timing is not None else None)
+            for _ in range(k):
+                pipe.step(pay_sub[0])
+            pipe.finish()
         else:
             for _ in range(k):
                 step()
@@ -680,7 +789,10 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         sm_ms = sum(e0.elapsed_time(e1) for e0, e1 in sb.sm_timing) / args.steps
     sb.sm_timing = None
     elapsed = max_over_ranks(elapsed, world, dev)
-    xms = timer.elapsed_ms() / args.steps if world > 1 else 0.0
+    if world > 1 and overlap:   # spans of the exchanges on the pipes' main streams
+        xms = sum(a.elapsed_time(b) for a, b in xspans) / args.steps
+    else:
+        xms = timer.elapsed_ms() / args.steps if world > 1 else 0.0
     timer.timing = False
     # per-rank record of the exchange: world, backend, and per collective the
     # calls and bytes this rank sent during the timed steps (rank 0 prints all)
@@ -736,7 +848,10 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                    # hbbft_amd.sharded.rank_footprint, torch buffers + reconstruct
                    # workspace bound), against 288 GB of HBM per MI355X
                    "hbm_footprint_per_rank": footprint_summary(n, count, plen,
-                                                               2 if overlap else 1, npipe)},
+                                                               2 if overlap else 1, npipe),
+                   "state_machine_group": ("its own process group (one RCCL communicator for the "
+                                           "rounds' all-gathers, one for the data plane)"
+                                           if sm_ex is not None else None)},
         "exchange": {"ms_per_step": xms, "bytes_per_step_per_gpu": xbytes,
                      "GBps_per_gpu": xbytes / (xms / 1e3) / 1e9 if xms > 0 else None,
                      "backend": ex.backend, "per_rank": per_rank},
@@ -747,24 +862,41 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
         **({"stages_note": "%d step pipelines run side by side: a stage's span includes the "
                            "other pipelines' kernels (--vpipes 1 gives the serial split)" % npipe}
            if npipe > 1 else {}),
+        # the same string at every world size (the world shows in config.parallelism)
         "state_machine_schedule": ("step i's rounds on a second HIP stream beside step i + 1's "
                                    "data plane (two state-machine slots); every step's rounds "
                                    "complete inside the timed region" if overlap else
-                                   "after each step's decode, in lockstep over the ranks")
+                                   "after each step's decode")
                                   + ("; %d step pipelines side by side on their own streams, "
                                      "step i on pipe i %% %d (stage times overlap)" % (npipe, npipe)
                                      if npipe > 1 else ""),
     }
 
 
+_SM_EX = []
+
+
+def sm_exchange():
+    """The state machine's own process group (created once, collectively, by
+    every rank in the same order): its per-round all-gathers run on a side
+    stream beside the data plane's collectives, and a communicator of their
+    own keeps the two from interleaving differently on different ranks."""
+    import torch.distributed as dist
+
+    from hbbft_amd.sharded import DistExchange
+    if not _SM_EX:
+        _SM_EX.append(DistExchange(dist.new_group(list(range(dist.get_world_size())))))
+    return _SM_EX[0]
+
+
 def footprint_summary(n, count, plen, sm_slots=1, pipes=1):
     from hbbft_amd.sharded import HBM_PER_GPU, rank_footprint
     out = {}
     for g in (1, 2, 4, 8):
-        # (two state-machine slots and the step pipelines only where they are
-        # used: one rank)
-        fp = rank_footprint(n, count, plen, g, 0, sm_slots=sm_slots if g == 1 else 1)
-        k = pipes if g == 1 else 1
+        # the schedule is the same at every world size: sm_slots state-machine
+        # slots per pipeline, `pipes` pipelines
+        fp = rank_footprint(n, count, plen, g, 0, sm_slots=sm_slots)
+        k = pipes
         out["G%d" % g] = {"bytes": k * fp["total_bytes"], "frac_of_288GB": k * fp["frac_of_hbm"],
                           "echo_slab_bytes": fp["buffers"].get("echo_sh", fp["buffers"]["slab"])}
     assert all(v["bytes"] < HBM_PER_GPU for v in out.values()), out
@@ -975,7 +1107,8 @@ def main():
     vcount = args.vcount or vcount
     head = vobj = None
     if args.mode in ("instances", "both"):
-        head = run_instances(args, n, plen, count, erase, rank, world, dev, local)
+        head = run_instances(args, n, plen, count, erase, rank, world, dev, local,
+                             encode_merkle=args.config == "cfg2")
     if args.mode in ("validators", "both"):
         torch.cuda.empty_cache()
         if head is None:
@@ -1001,6 +1134,24 @@ def main():
         except Exception as e:  # noqa: BLE001  (secondary object: keep the headline line)
             v4 = {"error": "%s: %s" % (type(e).__name__, e)}
             print("bench: cfg4 validator-sharded run failed: %r" % (e,), file=sys.stderr)
+
+    # BASELINE's other GPU configs ride along the default cfg3 line, instance-
+    # sharded over the ranks like the headline, so the driver's 1- and
+    # 8-GPU runs measure them: cfg2 (N=16, 1 MiB x 4096, with its own
+    # encode+Merkle metric) and cfg5 (N=250, 4 MiB, worst-case decode)
+    riders = {}
+    if args.mode == "both" and args.config == "cfg3" and not args.no_riders:
+        for cfg in ("cfg2", "cfg5"):
+            torch.cuda.empty_cache()
+            n_, plen_, cnt_, er_, _ = CONFIGS[cfg]
+            try:
+                riders[cfg] = run_instances(args, n_, plen_, args.rider_count or cnt_, er_, rank,
+                                            world, dev, local,
+                                            config=cfg, streams=1, leaf_reuse=False,
+                                            encode_merkle=cfg == "cfg2")
+            except Exception as e:  # noqa: BLE001  (secondary object: keep the headline line)
+                riders[cfg] = {"error": "%s: %s" % (type(e).__name__, e)}
+                print("bench: %s instance run failed: %r" % (cfg, e), file=sys.stderr)
 
     f4 = None
     if args.f4_checks > 0:
@@ -1046,6 +1197,8 @@ def main():
                 line["validators"] = vobj
             if v4 is not None:
                 line["validators_cfg4"] = v4
+            for cfg, obj in riders.items():
+                line[cfg] = obj
             if f4 is not None:
                 line["threshold_decrypt"] = f4
         else:

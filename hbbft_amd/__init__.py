@@ -133,6 +133,7 @@ def lib():
         "hbrbc_jit_decode_variant_file_name": (ctypes.c_int, [_S, _S, _P, _S, _S, ctypes.c_int,
                                                               ctypes.c_char_p, _S]),
         "hbrbc_unframe_fused": (ctypes.c_int, [_P, _S, _S, _S]),
+        "hbrbc_drop_rows": (ctypes.c_int, [_P, _P, _S, _S, _S, _S, _P, _S, ctypes.c_uint8, _P]),
         "hbrbc_pairing_workspace_size": (_S, [_S]),
         "hbrbc_g2_prepared_size": (_S, [_S]),
         "hbrbc_g2_prepare": (ctypes.c_int, [_P, _S, _P, _P]),
@@ -685,6 +686,13 @@ class RbcBatch:
         _check(lib().hbrbc_reconstruct_batch(self.coding.handle, _ptr(slab), S, slab.stride(1),
                                              slab.stride(0), _ptr(present), slab.shape[0],
                                              _ptr(status), self._stream(stream)))
+
+    def drop_rows(self, slab, present, fill=0xA5, stream=None):
+        """Overwrite every row with present == 0 (whole slot) with `fill`: the
+        rows a receiver never got (hbrbc_drop_rows); slab [count][n][stride]."""
+        _check(lib().hbrbc_drop_rows(self.coding.handle, _ptr(slab), slab.stride(1), 0, 0,
+                                     slab.stride(0), _ptr(present), slab.shape[0], fill,
+                                     self._stream(stream)))
 
     def unframe_fused(self, S, payload_stride, rows_per_block=0):
         """Whether decode writes the payload from the reconstruct kernel (same

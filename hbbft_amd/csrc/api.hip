@@ -1624,6 +1624,22 @@ int hbrbc_decode_batch(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, size_t s
                              payload_stride, payload_len_out, status_out, stream);
 }
 
+int hbrbc_drop_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_stride, size_t rows_per_block,
+                    size_t block_stride, size_t inst_stride, const uint8_t *present, size_t count,
+                    uint8_t fill, void *stream) {
+    if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");
+    if (count == 0) return HBRBC_OK;
+    if (!present) return fail(HBRBC_E_INVALID_ARG, "null present flags");
+    int st = check_slab(shards, shard_stride, shard_stride, inst_stride, c->n, count,
+                        rows_per_block, block_stride);
+    if (st) return st;
+    HB_HIP(hipSetDevice(c->device));
+    HB_HIP(launch_drop_rows(shards, shard_stride,
+                            make_rows(c->n, shard_stride, rows_per_block, block_stride),
+                            inst_stride, c->n, count, present, fill, pick(c, stream)));
+    return HBRBC_OK;
+}
+
 // ---------------------------------------------------- decode-matrix cache --
 int hbrbc_decode_cache_clear(hbrbc_ctx *c) {
     if (!c) return fail(HBRBC_E_INVALID_ARG, "null context");

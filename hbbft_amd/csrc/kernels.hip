@@ -1792,4 +1792,39 @@ hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, const RowMap 
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------- drop rows --
+// What a receiver does not hold: every row of instance i with present == 0
+// (the shards decode_from_shards gets as None, broadcast.rs:566-571) is
+// overwritten with `fill` over its whole slot, so a decode that follows
+// really rebuilds it.  One workgroup per instance; the row loop is uniform
+// (the present flags are read once into LDS), stores are 16-byte and
+// coalesced along the row.
+__global__ __launch_bounds__(kBlock) void drop_rows_kernel(
+    uint8_t *__restrict__ shards, uint32_t slot16, RowMap rows, size_t inst_stride,
+    uint32_t n, const uint8_t *__restrict__ present, uint32_t fill) {
+    __shared__ uint8_t pres[256];
+    const size_t inst = blockIdx.x;
+    for (uint32_t j = threadIdx.x; j < n; j += kBlock) pres[j] = present[inst * n + j];
+    __syncthreads();
+    const uint4 v = make_uint4(fill, fill, fill, fill);
+    uint8_t *ib = shards + inst * inst_stride;
+    for (uint32_t j = 0; j < n; ++j) {
+        if (pres[j]) continue;
+        uint4 *row = reinterpret_cast<uint4 *>(ib + rows.off(j));
+        for (uint32_t c = threadIdx.x; c < slot16; c += kBlock) row[c] = v;
+    }
+}
+
+hipError_t launch_drop_rows(uint8_t *shards, size_t shard_stride, const RowMap &rows,
+                            size_t inst_stride, size_t n, size_t count, const uint8_t *present,
+                            uint8_t fill, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (n > 256 || count > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t f4 = 0x01010101u * fill;
+    hipLaunchKernelGGL(drop_rows_kernel, dim3((unsigned)count), dim3(kBlock), 0, s, shards,
+                       (uint32_t)(shard_stride / 16), rows, inst_stride, (uint32_t)n, present, f4);
+    return hipGetLastError();
+}
+
 }  // namespace hbrbc
+

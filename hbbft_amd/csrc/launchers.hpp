@@ -199,6 +199,12 @@ hipError_t launch_unframe(const uint8_t *shards, size_t shard_len, const RowMap 
                           const uint32_t *plen, const int32_t *status, uint8_t *payload_out,
                           size_t payload_stride, hipStream_t s);
 
+// Overwrite every row with present == 0 (whole slot, 16-byte stores) with
+// `fill`: the rows a receiver never got (hbrbc_drop_rows).
+hipError_t launch_drop_rows(uint8_t *shards, size_t shard_stride, const RowMap &rows,
+                            size_t inst_stride, size_t n, size_t count, const uint8_t *present,
+                            uint8_t fill, hipStream_t s);
+
 // bincode wire format of broadcast::Message (wire.hip).
 struct WireEncodeArgs {
     uint32_t variant;           // 0 Value, 1 Echo

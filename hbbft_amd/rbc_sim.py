@@ -401,11 +401,13 @@ class LocalRounds:
     def _ctx(self):
         return torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
 
-    def launch(self, fresh=True):
+    def launch(self):
+        """Every run starts from fresh nodes: the per-round counts (hist) are
+        accumulated by the kernel, and the inbox of the rounds after the last
+        quiescent one still holds records, so a run never continues another."""
         with self._ctx():
-            if fresh:
-                for sm in self.ranks:
-                    sm.reset()
+            for sm in self.ranks:
+                sm.reset()
             self._enqueue(0, min(self.max_rounds, ROUND_BATCH))
         return self
 
@@ -433,45 +435,51 @@ class _nullctx:
         return False
 
 
-def run_rounds(ranks, exchange=None, max_rounds=64, fresh=True):
+def run_rounds(ranks, exchange=None, max_rounds=64):
     """Drive the state machine until no node emits a message.  `ranks`: the
     StateMachineRank objects of this process -- all virtual ranks of one
     topology for a loopback run (exchange None), or independent objects of
     this rank (e.g. pipelined sub-batches) with a DistExchange / SoloExchange
     `exchange`, whose world they share.  Returns the number of rounds
     (LocalRounds / _run_rounds_dist: batches of rounds, one read-back per
-    batch)."""
+    batch).  Every run starts from fresh nodes (StateMachineRank.reset)."""
     if exchange is not None and exchange.world > 1:
-        max_rounds = min(max_rounds, min(sm.max_rounds for sm in ranks))
-        if fresh:
-            for sm in ranks:
-                sm.reset()
         return _run_rounds_dist(ranks, exchange, max_rounds)
-    return LocalRounds(ranks, loopback=exchange is None, max_rounds=max_rounds).launch(fresh).wait()
+    return LocalRounds(ranks, loopback=exchange is None, max_rounds=max_rounds).launch().wait()
 
 
-def _run_rounds_dist(ranks, ex, max_rounds):
-    """run_rounds over a process group: ONE all-gather per round carries every
-    sub-batch's records and counts plus each one's emitted count and overflow
-    flag (instead of an all-reduce and two all-gathers per sub-batch); the
-    next round's `active` is the device sum of the gathered counts, and the
-    gathered tails of a batch of rounds are read back once."""
-    dev = ranks[0].device
-    parts = [(sm.out.numel(), sm.out_count.numel()) for sm in ranks]
-    k = len(ranks)
-    body = sum(a + b for a, b in parts)
-    send = torch.zeros(body + k + 1, dtype=torch.int32, device=dev)
-    recv = torch.empty((ex.world, body + k + 1), dtype=torch.int32, device=dev)
-    tails = torch.zeros((max_rounds, ex.world, k + 1), dtype=torch.int32, device=dev)
-    act = torch.zeros(max_rounds + 1, dtype=torch.int32, device=dev)
-    r = 0
-    while r < max_rounds:
-        hi = min(max_rounds, r + ROUND_BATCH)
+class DistRounds:
+    """run_rounds over a process group, split into enqueue and read-back like
+    LocalRounds so a caller can overlap the rounds with other work (the
+    validator-sharded step pipelines at world > 1, sharded.OverlapPipe):
+    `launch()` enqueues the first ROUND_BATCH rounds on `stream` and returns;
+    `wait()` reads the gathered tails back once per batch (synchronising that
+    stream only), enqueues further batches until quiescence and returns the
+    number of rounds.  ONE all-gather per round carries every sub-batch's
+    records and counts plus each one's emitted count and overflow flag
+    (instead of an all-reduce and two all-gathers per sub-batch); the next
+    round's `active` is the device sum of the gathered counts.  Every rank
+    reads the same tails, so every rank makes the same enqueue decisions and
+    the collectives of `ex` stay in the same order on every rank.  Give `ex`
+    a process group of its own when other collectives (the data plane's) run
+    concurrently on another stream."""
+
+    def __init__(self, ranks, ex, max_rounds=64, stream=None):
+        self.ranks, self.ex, self.stream = ranks, ex, stream
+        self.max_rounds = min(max_rounds, min(sm.max_rounds for sm in ranks))
+        self.next = 0
+
+    def _ctx(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
+
+    def _enqueue(self, r, hi):
+        ranks, ex = self.ranks, self.ex
+        send, recv, body, k = self.send, self.recv, self.body, len(ranks)
         for rr in range(r, hi):
             for sm in ranks:
-                sm.round(rr, active=None if rr == 0 else act[rr])
+                sm.round(rr, active=None if rr == 0 else self.act[rr])
             off = 0
-            for sm, (a, b) in zip(ranks, parts):
+            for sm, (a, b) in zip(ranks, self.parts):
                 send[off:off + a].copy_(sm.out.view(-1))
                 send[off + a:off + a + b].copy_(sm.out_count.view(-1))
                 off += a + b
@@ -479,22 +487,57 @@ def _run_rounds_dist(ranks, ex, max_rounds):
             send[body:body + k].copy_(hist[:, 0])
             send[body + k:].copy_(hist[:, 1].amax().view(1))
             ex.all_gather(recv, send, name="sm_round")
-            tails[rr].copy_(recv[:, body:])
-            act[rr + 1].copy_(recv[:, body:body + k].sum())
+            self.tails[rr].copy_(recv[:, body:])
+            self.act[rr + 1].copy_(recv[:, body:body + k].sum())
             off = 0
-            for sm, (a, b) in zip(ranks, parts):
+            for sm, (a, b) in zip(ranks, self.parts):
                 sm.inbox.view(ex.world, a).copy_(recv[:, off:off + a])
                 sm.inbox_count.view(ex.world, b).copy_(recv[:, off + a:off + a + b])
                 off += a + b
-        t = tails[r:hi].cpu()                                       # [rounds][world][k + 1]
-        # every rank's per-round totals (records of all ranks, overflow of any)
-        h = torch.stack([t[:, :, :k].sum(dim=1).sum(dim=1), t[:, :, k].amax(dim=1)], dim=1)
-        own = t[:, ex.rank, :k].transpose(0, 1)                     # [k][rounds]
-        done = _check_batch(ranks, h.unsqueeze(0), r, own=own)
-        if done is not None:
-            return done
-        r = hi
-    raise RuntimeError("state machine did not quiesce in %d rounds" % max_rounds)
+        self.next = hi
+
+    def launch(self):
+        """Fresh nodes (every run), then the first batch of rounds."""
+        ranks, ex = self.ranks, self.ex
+        dev = ranks[0].device
+        with self._ctx():
+            for sm in ranks:
+                sm.reset()
+            self.parts = [(sm.out.numel(), sm.out_count.numel()) for sm in ranks]
+            k = len(ranks)
+            self.body = sum(a + b for a, b in self.parts)
+            self.send = torch.zeros(self.body + k + 1, dtype=torch.int32, device=dev)
+            self.recv = torch.empty((ex.world, self.body + k + 1), dtype=torch.int32, device=dev)
+            self.tails = torch.zeros((self.max_rounds, ex.world, k + 1), dtype=torch.int32,
+                                     device=dev)
+            self.act = torch.zeros(self.max_rounds + 1, dtype=torch.int32, device=dev)
+            self._enqueue(0, min(self.max_rounds, ROUND_BATCH))
+        return self
+
+    def wait(self):
+        ranks, ex, k = self.ranks, self.ex, len(self.ranks)
+        r = 0
+        with self._ctx():
+            while True:
+                hi = self.next
+                t = self.tails[r:hi].cpu()                          # [rounds][world][k + 1]
+                # every rank's per-round totals (records of all ranks, overflow of any)
+                h = torch.stack([t[:, :, :k].sum(dim=1).sum(dim=1), t[:, :, k].amax(dim=1)], dim=1)
+                own = t[:, ex.rank, :k].transpose(0, 1)             # [k][rounds]
+                done = _check_batch(ranks, h.unsqueeze(0), r, own=own)
+                if done is not None:
+                    return done
+                if hi >= self.max_rounds:
+                    raise RuntimeError("state machine did not quiesce in %d rounds"
+                                       % self.max_rounds)
+                self._enqueue(hi, min(self.max_rounds, hi + ROUND_BATCH))
+                r = hi
+
+
+def _run_rounds_dist(ranks, ex, max_rounds):
+    """run_rounds over a process group (DistRounds, enqueued and read back in
+    one call)."""
+    return DistRounds(ranks, ex, max_rounds).launch().wait()
 
 
 def simulate(scn, world=1, device=0, max_out=24, max_faults=None):

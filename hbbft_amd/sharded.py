@@ -467,18 +467,19 @@ class ShardedBroadcast:
         st, rpb, bst, ist = self._prop_layout()
         rb.frame_encode_rows(payloads, self.plen, self.slab, C, st, rpb, bst, ist)
 
-    def rest_phase(self, ex):
+    def rest_phase(self, ex, xspans=None):
         """Everything of a step after the encoder: tree, proofs, exchanges,
         validation, decode (which leaves the state machine's outcomes in the
-        current slot)."""
+        current slot).  xspans: a list receiving (start, end) timing events
+        around each exchange on the current stream (world > 1)."""
         rb, S, C = self.rb, self.S, self.count
         st, rpb, bst, ist = self._prop_layout()
         rb.merkle_rows(self.slab, S, C, st, rpb, bst, ist, self.nodes)
         rb.proofs(self.nodes, self.digests, self.ndig)
         self.pack_value()
-        self.exchange_value(ex)
+        _timed(xspans, self.world, lambda: self.exchange_value(ex))
         self.validate_values()
-        self.exchange_echo(ex)
+        _timed(xspans, self.world, lambda: self.exchange_echo(ex))
         self.validate_echoes()
         self.decode()
 
@@ -516,6 +517,19 @@ class ShardedBroadcast:
             "state_machine_rounds": self.sm_rounds,
             "state_machine_messages": self.sm.records,
         }
+
+
+def _timed(spans, world, fn):
+    """fn() between two timing events on the current stream when spans is a
+    list and the exchange moves data (world > 1)."""
+    if spans is None or world == 1:
+        return fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    r = fn()
+    b.record()
+    spans.append((a, b))
+    return r
 
 
 HBM_PER_GPU = 288 * 10**9   # MI355X HBM3E
@@ -639,31 +653,46 @@ def pipelined_step(subs, payloads, ex, timer):
 
 
 class OverlapPipe:
-    """The steps of one rank with no process group (world 1), the state
-    machine of step i on the `side` stream beside the data plane of step
-    i + 1 on the `main` stream (sb built with sm_slots=2; the slots
-    alternate).  The rounds are latency-bound at low occupancy, the data
-    plane's sponges issue-bound: side by side the GPU fills the one's idle
-    issue slots with the other's work.  Step i's rounds start after step
-    i + 1's encoder: the LDS-staged encoder needs 48 KB of LDS per workgroup
-    and ran at half speed beside the rounds' LDS images (validator cfg4:
-    encode 0.69 -> 1.50 ms), the sponge kernels use none.  `timing`: a list
-    that receives (start, end) events of each step's rounds on the side
-    stream."""
+    """The steps of one rank, the state machine of step i on the `side`
+    stream beside the data plane of step i + 1 on the `main` stream (sb
+    built with sm_slots=2; the slots alternate).  The rounds are
+    latency-bound at low occupancy, the data plane's sponges issue-bound:
+    side by side the GPU fills the one's idle issue slots with the other's
+    work.  Step i's rounds start after step i + 1's encoder: the LDS-staged
+    encoder needs 48 KB of LDS per workgroup and ran at half speed beside the
+    rounds' LDS images (validator cfg4: encode 0.69 -> 1.50 ms), the sponge
+    kernels use none.  `timing`: a list that receives (start, end) events of
+    each step's rounds on the side stream.
 
-    def __init__(self, sb, ex, side, main=None, timing=None):
-        assert len(sb.sms) == 2 and ex.world == 1
+    world > 1 (ex a DistExchange): the data plane's Value all-to-all and Echo
+    all-gather run on `main` over `ex`; the rounds' per-round all-gathers
+    (rbc_sim.DistRounds) run on `side` over `sm_ex`, which must hold a
+    process group of its own (dist.new_group: its own RCCL communicator),
+    so the two streams' collectives never interleave in a different order
+    on different ranks.  Every rank enqueues the same collectives in the
+    same order on each group, and a step's host read-back of the rounds of
+    the step before waits only after this step's data plane is enqueued on
+    every rank, so no rank can block a collective another rank waits for."""
+
+    def __init__(self, sb, ex, side, main=None, timing=None, sm_ex=None, xspans=None):
+        assert len(sb.sms) == 2
+        if ex.world > 1 and (sm_ex is None or getattr(sm_ex, "group", None) is None
+                             or sm_ex.group is getattr(ex, "group", None)):
+            raise ValueError("world > 1: the overlapped state machine needs its own process "
+                             "group (sm_ex = DistExchange(dist.new_group()))")
         self.sb, self.ex, self.side = sb, ex, side
+        self.sm_ex = sm_ex if sm_ex is not None else ex
         self.main = main if main is not None else torch.cuda.current_stream()
         # the buffers and payloads were written on the caller's stream
         self.main.wait_stream(torch.cuda.current_stream())
         side.wait_stream(torch.cuda.current_stream())
         self.timing = timing
+        self.xspans = xspans
         self.steps = 0
         self.prev_ready = None   # step i - 1's data plane is done (its outcomes are in)
 
     def _launch(self, slot, ready, after):
-        from .rbc_sim import LocalRounds
+        from .rbc_sim import DistRounds, LocalRounds
         side = self.side
         side.wait_event(ready)
         if after is not None:
@@ -673,7 +702,12 @@ class OverlapPipe:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record(side)
             self.timing.append(ev)
-        return slot, LocalRounds([self.sb.sms[slot]], loopback=False, stream=side).launch(), ev
+        sms = [self.sb.sms[slot]]
+        if self.sm_ex.world > 1:
+            rounds = DistRounds(sms, self.sm_ex, stream=side).launch()
+        else:   # one rank: its nodes only talk to themselves
+            rounds = LocalRounds(sms, loopback=False, stream=side).launch()
+        return slot, rounds, ev
 
     def _drain(self, p):
         slot, lr, ev = p
@@ -699,7 +733,7 @@ class OverlapPipe:
             running = None
             if self.prev_ready is not None:   # step i - 1's rounds, after step i's encoder
                 running = self._launch((i - 1) % 2, self.prev_ready, after_encode)
-            sb.rest_phase(self.ex)
+            sb.rest_phase(self.ex, self.xspans)
             self.prev_ready = torch.cuda.Event()
             self.prev_ready.record(self.main)
         if running is not None:
@@ -719,17 +753,19 @@ class OverlapPipe:
         cur.wait_stream(self.side)
 
 
-def overlapped_steps(sb, payloads, ex, steps, side, timing=None):
+def overlapped_steps(sb, payloads, ex, steps, side, timing=None, sm_ex=None):
     """`steps` steps of one OverlapPipe on the current stream."""
-    pipe = OverlapPipe(sb, ex, side, timing=timing)
+    pipe = OverlapPipe(sb, ex, side, timing=timing, sm_ex=sm_ex)
     for _ in range(steps):
         pipe.step(payloads)
     pipe.finish()
 
 
 def interleaved_steps(pipes, payloads, steps):
-    """`steps` steps over several OverlapPipes on their own streams (world 1),
-    step i on pipes[i % len(pipes)]: the pipes' data planes run side by side,
+    """`steps` steps over several OverlapPipes on their own streams, step i
+    on pipes[i % len(pipes)] (at world > 1 every rank steps the pipes in the
+    same order, so each group's collectives keep one order across ranks):
+    the pipes' data planes run side by side,
     so a sponge launch of one (4,096 lockstep waves at validator cfg3, one
     residency round) shares the SIMDs with another pipe's kernels instead of
     running in one synchronous round, and one pipe's rebuilt-row list and

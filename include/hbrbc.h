@@ -274,6 +274,17 @@ int hbrbc_decode_rows(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_len, size_t 
                       int known_leaves, uint8_t *payload_out, size_t payload_stride,
                       uint32_t *payload_len_out, int32_t *status_out, void *stream);
 
+/* A receiver holds only the rows it got: every row of instance i with
+ * present[i*n + j] == 0 (the shards decode_from_shards gets as None,
+ * broadcast.rs:566-571) is overwritten with `fill` over its whole slot
+ * (shard_stride bytes), in the plain or blocked layout.  A decode after it
+ * rebuilds those rows from the others; the benchmark drops the erased rows
+ * of every step this way so no timed decode starts from rows that still
+ * hold the right bytes.  n <= 256. */
+int hbrbc_drop_rows(hbrbc_ctx *ctx, uint8_t *shards, size_t shard_stride, size_t rows_per_block,
+                    size_t block_stride, size_t inst_stride, const uint8_t *present, size_t count,
+                    uint8_t fill, void *stream);
+
 /* ---- decode-matrix cache (rse's per-pattern decode-matrix LRU) ----------- */
 /* Every reconstruct/decode call looks each instance's present pattern up in a
  * device hash table: the first instance of a new pattern computes inv(M[first

@@ -63,13 +63,22 @@ def test_bench_line_small():
     none of them an error."""
     import json
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--count", "512",
-                        "--vcount", "256", "--steps", "2", "--warmup", "2", "--no-cpu",
+                        "--vcount", "256", "--rider-count", "64", "--steps", "2", "--warmup", "2",
+                        "--no-cpu",
                         "--f4-checks", "4096", "--f4-steps", "1"],
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["value"] > 0 and line["n_gpus"] == 1 and line["config"]["instances_per_gpu"] == 512
-    assert line["leaf_reuse"]["value"] > 0
+    assert line["leaf_reuse"]["value"] > 0 and line["leaf_reuse"]["verified_last_timed_step"]
+    assert line["stages_ms_per_step"]["erase"] > 0
+    # BASELINE's cfg2 (with its encode+Merkle rate) and cfg5 ride along
+    for key, n in (("cfg2", 16), ("cfg5", 250)):
+        v = line[key]
+        assert "error" not in v, v.get("error")
+        assert v["value"] > 0 and v["config"]["n"] == n and v["verified_last_timed_step"]
+        assert v["roofline"]["kernel"] and v["ms_per_step"] > 0
+    assert line["cfg2"]["encode_merkle"]["value"] > line["cfg2"]["value"]
     for key in ("validators", "validators_cfg4"):
         v = line[key]
         assert "error" not in v, v.get("error")

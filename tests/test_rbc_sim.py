@@ -367,6 +367,13 @@ class _FakeSm:
         self.last = 2 if (rank, b) != (1, 1) else 3
         self.ran = []
 
+    def reset(self):
+        self.hist.zero_()
+        self.out_count.zero_()
+        self.inbox_count.zero_()
+        self.records = 0
+        self.ran = []
+
     def round(self, r, active=None):
         if active is not None and int(active) == 0:
             return
@@ -421,3 +428,42 @@ def test_gloo_fused_round_exchange():
     for p in procs:
         p.join(60)
     assert res == {0: "ok", 1: "ok"}, res
+
+
+class _FakeLocalSm(_FakeSm):
+    """_FakeSm with what LocalRounds drives on one rank: reset, emitted,
+    swap_local; like the kernel, a round ADDS its records into hist[r]."""
+
+    def __init__(self, **kw):
+        super().__init__(0, 1, 0, **kw)
+        self.last = 3
+
+    def round(self, r, active=None):
+        if active is not None and int(active) == 0:
+            return
+        self.ran.append(r)
+        emits = r <= self.last
+        self.out_count.fill_(1 if emits else 0)
+        self.hist[r, 0] += self.out_count.numel() if emits else 0   # accumulated, not stored
+
+    def emitted(self, r):
+        return self.hist[r, 0]
+
+    def swap_local(self):
+        self.inbox, self.out = self.out.unsqueeze(0), self.inbox[0]
+        self.inbox_count, self.out_count = self.out_count.unsqueeze(0), self.inbox_count[0]
+
+
+def test_local_rounds_run_twice_from_fresh_nodes():
+    """a second run of the same objects must not add to the first
+    run's per-round counts (the kernel accumulates into hist) or deliver the
+    records left after quiescence: every run starts from reset nodes and
+    gives the same rounds and record count."""
+    from hbbft_amd.rbc_sim import LocalRounds, run_rounds
+    sm = _FakeLocalSm()
+    first = LocalRounds([sm], loopback=False).launch().wait()
+    rec1, ran1 = sm.records, list(sm.ran)
+    second = LocalRounds([sm], loopback=False).launch().wait()
+    assert (first, sm.records, sm.ran) == (second, rec1, ran1) == (5, 4 * sm.out_count.numel(),
+                                                                   [0, 1, 2, 3, 4])
+    assert run_rounds([sm]) == 5 and sm.records == rec1

@@ -127,6 +127,192 @@ def test_gloo_value_all_to_all_and_echo_all_gather(n, world):
     assert res == {r: "ok" for r in range(world)}, res
 
 
+# ---- the overlapped schedule at world > 1, on CPU (gloo, fake kernels) ----
+class _NoStream:
+    """torch.cuda stream / event stand-ins: on the CPU every op is already
+    ordered, so the schedule's control flow and collectives run unchanged."""
+
+    def __init__(self, *a, **k):
+        pass
+
+    def wait_event(self, e):
+        pass
+
+    def wait_stream(self, s):
+        pass
+
+    def record(self, stream=None):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _no_cuda_streams():
+    torch.cuda.Stream = _NoStream
+    torch.cuda.Event = _NoStream
+    torch.cuda.stream = _NoStream
+    torch.cuda.current_stream = lambda *a: _NoStream()
+
+
+class _FakeSm:
+    """A StateMachineRank stand-in whose rounds depend on the data plane's
+    outcomes (`ok`) and on every rank's records: each round adds the
+    gathered records to `acc` and emits ok * (r + 1) + rank for 3 rounds."""
+
+    def __init__(self, rank, world, count):
+        self.rank, self.count = rank, count
+        self.device = torch.device("cpu")
+        self.max_rounds, self.max_out = 16, 1
+        self.ok = torch.zeros(count, dtype=torch.int32)
+        self.out = torch.zeros((count, 1, 1, 2), dtype=torch.int32)
+        self.out_count = torch.zeros((count, 1), dtype=torch.int32)
+        self.inbox = torch.zeros((world, count, 1, 1, 2), dtype=torch.int32)
+        self.inbox_count = torch.zeros((world, count, 1), dtype=torch.int32)
+        self.hist = torch.zeros((16, 2), dtype=torch.int32)
+        self.acc = torch.zeros(count, dtype=torch.int64)
+        self.records = 0
+
+    def reset(self):
+        self.hist.zero_()
+        self.out_count.zero_()
+        self.inbox_count.zero_()
+        self.acc.zero_()
+        self.records = 0
+
+    def round(self, r, active=None):
+        if active is not None and int(active) == 0:
+            return
+        if r > 0:
+            self.acc += (self.inbox[:, :, 0, 0, 0] * self.inbox_count[:, :, 0]).sum(0)
+        emit = r < 3
+        self.out[:, 0, 0, 0] = self.ok * (r + 1) + self.rank
+        self.out_count.fill_(1 if emit else 0)
+        self.hist[r, 0] += self.count if emit else 0
+
+
+class _FakeShardedBroadcast:
+    """The data plane of a step: Value / Echo collectives over `ex` whose
+    results feed the current slot's state machine; `history` = every
+    finished step's outputs, in step order."""
+
+    def __init__(self, rank, world, count):
+        self.rank, self.world, self.count = rank, world, count
+        self.sms = [_FakeSm(rank, world, count) for _ in range(2)]
+        self.slot, self.sm_rounds, self.sm_timing = 0, 0, None
+        self.history = []
+
+    @property
+    def sm(self):
+        return self.sms[self.slot]
+
+    def encode_phase(self, payloads):
+        self.pay = payloads.clone()
+
+    def rest_phase(self, ex, xspans=None):
+        g = torch.zeros((self.world, self.count), dtype=torch.int32)
+        ex.all_gather(g, self.pay, name="value")                       # Value / Echo fan-out
+        roots = torch.zeros((self.world, self.count), dtype=torch.int32)
+        ex.all_to_all(roots, (g * (self.rank + 2)).contiguous(), name="echo")
+        self.sm.ok.copy_(g.sum(0) + roots.sum(0))
+
+    def data_step(self, payloads, ex):
+        self.encode_phase(payloads)
+        self.rest_phase(ex)
+
+    def finish(self):
+        self.history.append(self.sm.acc.clone())
+
+
+def _gloo_schedule_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from hbbft_amd.sharded import (OverlapPipe, interleaved_steps, run_state_machines)
+    _no_cuda_streams()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ex = DistExchange()
+        sm_ex = DistExchange(dist.new_group(list(range(world))))
+        count, steps = 5, 5
+
+        def pay(i):
+            return torch.arange(count, dtype=torch.int32) * 7 + 100 * i + 13 * rank
+        # serial: data plane, then the rounds over the data group, step by step
+        ser = _FakeShardedBroadcast(rank, world, count)
+        for i in range(steps):
+            ser.data_step(pay(i), ex)
+            ser.sm_rounds = run_state_machines([ser], ex)
+        # overlapped: step i's rounds (own group) beside step i + 1's data plane
+        ov = _FakeShardedBroadcast(rank, world, count)
+        pipe = OverlapPipe(ov, ex, _NoStream(), main=_NoStream(), sm_ex=sm_ex)
+        for i in range(steps):
+            pipe.step(pay(i))
+        pipe.finish()
+        # two pipelines, step i on pipe i % 2
+        pp = [_FakeShardedBroadcast(rank, world, count) for _ in range(2)]
+        pipes = [OverlapPipe(o, ex, _NoStream(), main=_NoStream(), sm_ex=sm_ex) for o in pp]
+        payl = [None, None]
+
+        class _Feed:   # interleaved_steps passes payloads[i % 2]: feed each step's own
+            def __getitem__(self, j):
+                return payl[j]
+        feed = _Feed()
+        for i in range(steps):
+            payl[i % 2] = pay(i)
+            pipes[i % 2].step(feed[i % 2])
+        for p in pipes:
+            p.finish()
+        inter = [pp[i % 2].history[i // 2] for i in range(steps)]
+        good = len(ser.history) == len(ov.history) == steps
+        good &= all(torch.equal(a, b) for a, b in zip(ser.history, ov.history))
+        good &= all(torch.equal(a, b) for a, b in zip(ser.history, inter))
+        good &= all(bool(h.any()) for h in ser.history) and ser.sm_rounds == ov.sm_rounds == 4
+        # the state machine's group refuses to be the data group
+        try:
+            OverlapPipe(_FakeShardedBroadcast(rank, world, count), ex, _NoStream(), sm_ex=ex)
+            good = False
+        except ValueError:
+            pass
+        q.put((rank, "ok" if good else "mismatch %s / %s / %s" % (
+            [h.tolist() for h in ser.history], [h.tolist() for h in ov.history],
+            [h.tolist() for h in inter])))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_overlapped_schedule_equals_serial(world):
+    """the overlapped validator schedule at world > 1 --
+    each step's state machine beside the next step's data plane, its
+    per-round all-gathers over a process group of their own, and two such
+    pipelines interleaved -- gives every step the same state-machine
+    outputs as the serial schedule (data plane, then the rounds, step by
+    step), on gloo over CPU with the kernels replaced by deterministic
+    stand-ins that depend on every rank's data and records."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_gloo_schedule_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {r: "ok" for r in range(world)}, res
+
+
 # ------------------------------------------------------------------ GPU ----
 def _payloads(seed, count, plen, dev):
     pay = np.stack([orc.gen_payload(seed, i, plen) for i in range(count)])
@@ -328,6 +514,28 @@ def _gloo_gpu_worker(rank, world, port, q):
                 good = good and np.array_equal(o[2 * s:2 * s + 2, :plen], exp)
             good = good and bool((sub.status.cpu() == 0).all())
         good = good and len(timer.spans) == 4 and timer.elapsed_ms() > 0
+        # the overlapped schedule the bench runs at every world size: two step
+        # pipelines, each step's state machine on a side stream beside the
+        # next step's data plane, its all-gathers over a group of their own;
+        # same payloads as the serial step above -> same outputs and flags
+        from hbbft_amd.sharded import OverlapPipe, interleaved_steps
+        sm_ex = DistExchange(dist.new_group(list(range(world))))
+        objs = [ShardedBroadcast(n, count, plen, rank, world, device=0, sm_slots=2)
+                for _ in range(2)]
+        xs = []
+        pipes = [OverlapPipe(o, DistExchange(), torch.cuda.Stream(o.device),
+                             main=torch.cuda.Stream(o.device), sm_ex=sm_ex, xspans=xs)
+                 for o in objs]
+        interleaved_steps(pipes, [t, t], 5)   # pipe 0: steps 0, 2, 4; pipe 1: 1, 3
+        torch.cuda.synchronize()
+        good = good and [p.steps for p in pipes] == [3, 2] and len(xs) == 2 * 5
+        for o in objs:
+            oo = o.out.cpu().numpy()
+            good = good and bool((o.status.cpu() == 0).all()) and bool(o.decided.cpu().all())
+            good = good and torch.equal(o.decided.cpu(), sb.decided.cpu())
+            good = good and o.sm_rounds == sb.sm_rounds
+            good = good and all(np.array_equal(oo[s * count:(s + 1) * count, :plen], allpay[s])
+                                for s in range(world))
         q.put((rank, "ok" if good else "mismatch %s" % sb.status.cpu().tolist()))
     except Exception as e:  # pragma: no cover
         q.put((rank, repr(e)))
@@ -337,6 +545,9 @@ def _gloo_gpu_worker(rank, world, port, q):
 
 @pytest.mark.gpu
 def test_sharded_two_ranks_gloo_on_one_gpu():
+    """Two ranks sharing cuda:0 over gloo: the serial step, the sub-batch
+    pipelined step, and the overlapped two-pipeline schedule (state machine
+    on its own process group), all against every rank's payloads."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -344,7 +555,7 @@ def test_sharded_two_ranks_gloo_on_one_gpu():
     procs = [ctx.Process(target=_gloo_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in procs)
+    res = dict(q.get(timeout=200) for _ in procs)
     for p in procs:
         p.join(60)
     assert res == {0: "ok", 1: "ok"}, res
@@ -367,6 +578,11 @@ def test_rank_footprint_fits_hbm(cfg, n, plen, count):
             fp = rank_footprint(n, count, plen, world, rank)
             assert fp["total_bytes"] < HBM_PER_GPU, (cfg, world, rank, fp["total_bytes"])
             assert all(v > 0 for v in fp["buffers"].values())
+            # the bench's schedule at every world size: two step pipelines,
+            # each with two state-machine slots
+            fp2 = rank_footprint(n, count, plen, world, rank, sm_slots=2)
+            assert fp2["total_bytes"] > fp["total_bytes"]
+            assert 2 * fp2["total_bytes"] < HBM_PER_GPU, (cfg, world, rank, fp2["total_bytes"])
         # the all-gathered echo slab grows with the world (every rank decodes all)
         assert fp["torch_bytes"] > prev
         prev = fp["torch_bytes"]

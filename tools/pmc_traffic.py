@@ -4,8 +4,11 @@
 MI355X_MICROARCH.md prescribes) of `bench.py --steps 1 --warmup 1`, as
 collected by tools/profile.sh.
 
-FETCH_SIZE / WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports half the bytes
-of a wide streaming read, so it is doubled.  Output (out.json): bytes per
+FETCH_SIZE / WRITE_SIZE are in KB.  FETCH_SIZE is divided by the calibration
+factor of the access pattern the kernel's loads follow
+(profiles/fetch_calibration.json, tools/fetch_calib.hip: raw counter bytes /
+known bytes on gfx950 -- 0.500 for 16- and 4-byte coalesced loads, 0.539 for
+the sponges' one-lane-per-row 8-byte loads); WRITE_SIZE measured exact (1.00).  Output (out.json): bytes per
 launch and per instance for every hbrbc kernel of every profiled config, and
 the "cfg:stage" -> bytes-per-instance map bench.py reads for roofline.traffic.
 With an SQ pass and a sponge geometry it also writes
@@ -38,6 +41,19 @@ def base(k):
     return k.split("<")[0]
 
 
+CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
+                     "fetch_calibration.json")
+
+
+def fetch_factor(k, calib):
+    """(raw / known factor, pattern name) of kernel k's loads."""
+    pats, kp = calib["patterns"], calib["kernel_pattern"]
+    for prefix, pat in kp.items():
+        if prefix != "default" and k.startswith(prefix):
+            return pats[pat]["fetch_factor"], pat
+    return pats[kp["default"]]["fetch_factor"], kp["default"]
+
+
 def per_launch(path, counter, scale):
     fs = glob.glob(path + "*/**/run_counter_collection.csv", recursive=True)
     if not fs:
@@ -59,6 +75,7 @@ def main():
     except (OSError, ValueError):
         doc = {}
     kernels_all, traffic = doc.get("kernels", {}), doc.get("traffic", {})
+    calib = json.load(open(CALIB))
     for spec in sys.argv[2:]:
         parts = spec.split(":")
         d, cfg, inst = parts[0], parts[1], int(parts[2])
@@ -66,8 +83,10 @@ def main():
         wr = per_launch(d + "/pmc_write", "WRITE_SIZE", 1024.0)
         kernels = {}
         for k in sorted(set(fe) | set(wr)):
-            f2 = 2.0 * fe.get(k, 0.0)
+            fac, pat = fetch_factor(k, calib)
+            f2 = fe.get(k, 0.0) / fac
             kernels[k] = {"fetch_raw_bytes": fe.get(k, 0.0), "fetch_corrected_bytes": f2,
+                          "fetch_factor": fac, "fetch_pattern": pat,
                           "write_bytes": wr.get(k, 0.0), "hbm_bytes": f2 + wr.get(k, 0.0),
                           "hbm_bytes_per_instance": (f2 + wr.get(k, 0.0)) / inst}
         kernels_all[cfg] = kernels
@@ -104,8 +123,10 @@ def main():
                                        "launch" % (os.path.basename(d), cfg, leaf[0], perms)}
                 json.dump(vdoc, open(vp, "w"), indent=1, sort_keys=True)
                 print("%s leaf_hash lane-ops per permutation: %.1f" % (cfg, ops))
-    traffic["_note"] = ("HBM bytes per instance per launch: (2 x FETCH_SIZE + WRITE_SIZE) x 1024 "
-                        "/ instances per launch (rocprofv3 --pmc passes, tools/profile.sh)")
+    traffic["_note"] = ("HBM bytes per instance per launch: (FETCH_SIZE / factor + WRITE_SIZE) x "
+                        "1024 / instances per launch (rocprofv3 --pmc passes, tools/profile.sh); "
+                        "factor = the calibrated raw/known ratio of the kernel's load pattern, "
+                        "profiles/fetch_calibration.json (tools/fetch_calib.hip)")
     json.dump({"kernels": kernels_all, "traffic": traffic}, open(out, "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
