@@ -722,11 +722,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
     const uint32_t L = *counter;
     const uint32_t lo = (uint32_t)((uint64_t)blockIdx.x * L / gridDim.x);
     const uint32_t nb = (uint32_t)((uint64_t)(blockIdx.x + 1) * L / gridDim.x) - lo;
+    uint32_t d[8];
+    if (nb > 384u) {
+        // more than one round and a pair-lane remainder per CU (a long list:
+        // ADVICE r4): every wave takes one-lane rounds of 512, so no wave
+        // idles while waves 0-3 run their rounds back to back
+        for (uint32_t t = threadIdx.x; t < nb; t += 512) {
+            const uint2 e = list[lo + t];
+            sha3_256_row(shards + e.x * inst_stride + rows.off(e.y), S, d);
+            store_digest(nodes + e.x * node_inst_stride + (size_t)e.y * 32, d);
+        }
+        return;
+    }
     const uint32_t rem = nb & 255u;
     const uint32_t np = rem <= 128u ? rem : 0u;   // pair-lane sponges of this block
     const uint32_t ns = nb - np;                  // one-lane sponges, in rounds of 256
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t d[8];
     if (wave < 4) {
         for (uint32_t t = threadIdx.x; t < ns; t += 256) {
             const uint2 e = list[lo + t];

@@ -54,14 +54,16 @@
 #define HB_SM_MERGE 1
 #endif
 // Global-records kernel: HB_SM_CONSTAS reads the inbox through the constant
-// address space (wave-uniform reads become scalar loads), HB_SM_UREC also
-// fetches a record's recipient-mask words as scalar loads (each lane picks its
-// word) instead of one vector load per record.
+// address space, so the wave-uniform reads (counts, record headers) are
+// scalar loads; the recipient-mask word is per lane (a wave holds nodes of
+// different 32-node words) and stays one vector load per record.  The typed
+// pointer goes all the way into sm_node (it was cast back to a
+// generic pointer there).  Checked in the ISA (hipcc -S, round 5, before and
+// after that change): the inbox loop of sm_round_grec_kernel<true> reads a
+// sender's count and each record header with s_load_dword and the mask word
+// with one global_load_dword (offset 4 / 8: words 1.. of the record).
 #ifndef HB_SM_CONSTAS
 #define HB_SM_CONSTAS 1
-#endif
-#ifndef HB_SM_UREC
-#define HB_SM_UREC 0
 #endif
 
 namespace hbrbc {
@@ -505,9 +507,11 @@ struct Sm {
         }
     }
 
-    __device__ __forceinline__ void deliver(int s, const uint32_t *r) {
-        const uint32_t kind = r[0] & 0xFFu, c0 = (r[0] >> 8) & 0xFFu;
-        const uint32_t j = (r[0] >> 16) & 0xFFu, t = (r[0] >> 24) & 0xFFu;
+    // r: the record (a generic pointer, or a constant-address-space one whose
+    // wave-uniform reads are scalar loads); only its header word is read here
+    __device__ __forceinline__ void deliver(int s, uint32_t h0) {
+        const uint32_t kind = h0 & 0xFFu, c0 = (h0 >> 8) & 0xFFu;
+        const uint32_t j = (h0 >> 16) & 0xFFu, t = (h0 >> 24) & 0xFFu;
         switch (kind) {
             case K_VALUE: {
                 // the proposer's Value to us: proof (value_root[me], me, value_tamper[me]);
@@ -566,7 +570,7 @@ struct SmLayout {
 // Handles one node's inbox of the round (or, in round 0, the proposer's
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
 // `inc(s)` sender s's record count, `recs(s)` its records.
-template <bool ONE, bool UREC = false, class InCount, class Recs>
+template <bool ONE, class InCount, class Recs>
 __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
                         InCount inc, Recs recs) {
@@ -616,31 +620,19 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     } else {
         m.drop = m.role == R_SILENT;
         const bool faker = a.fake_from[inst] == (uint8_t)me;
-        // this node's bit in a record's recipient mask; with wave-uniform
-        // records (UREC) every mask word is a scalar load and the lane picks
-        // its word in registers (one scalar load each instead of a vector
-        // load per record)
+        // this node's bit in a record's recipient mask (the record pointer
+        // keeps its address space: see HB_SM_CONSTAS)
         const int mw = me >> 5;
-        auto rbit = [&](const uint32_t *r) -> bool {
-            if constexpr (UREC) {
-                uint32_t word = 0;
-                for (int w = 0; w < W; ++w) {
-                    const uint32_t v = r[1 + w];
-                    word = w == mw ? v : word;
-                }
-                return (word >> (me & 31)) & 1u;
-            } else {
-                return m.bit(r + 1, me);
-            }
-        };
+        auto rbit = [&](auto r) -> bool { return (r[1 + mw] >> (me & 31)) & 1u; };
         for (int s = 0; s < n; ++s) {
             if (HB_SM_CACHE) m.em_focus(s >> 5);
             if (s == me) continue;   // targets never include the sender
             const uint32_t cnt = inc(s);
-            const uint32_t *rs = recs(s);
+            const auto rs = recs(s);
             for (uint32_t e = 0; e < cnt; ++e) {
-                const uint32_t *r = rs + (size_t)e * (1 + W);
-                const uint32_t k0 = r[0] & 0xFFu;
+                auto r = rs + (size_t)e * (1 + W);
+                uint32_t h0 = r[0];
+                const uint32_t k0 = h0 & 0xFFu;
                 bool hit = rbit(r);
                 // An Echo and an EchoHash of the same sender in a row whose
                 // targets do not overlap at this node (handle_value emits
@@ -653,22 +645,24 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
                 // records with scalar loads.
                 if (HB_SM_MERGE) {
                     bool pair = false, hit2 = false;
-                    const uint32_t *r2 = r + (1 + W);
+                    uint32_t h1 = 0;
+                    const auto r2 = r + (1 + W);
                     if ((k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
-                        const uint32_t k1 = r2[0] & 0xFFu;
+                        h1 = r2[0];
+                        const uint32_t k1 = h1 & 0xFFu;
                         hit2 = rbit(r2);
                         pair = (k1 == K_ECHO || k1 == K_ECHO_HASH) && k1 != k0 && !(hit && hit2);
                     }
                     if (__all(pair)) {
                         ++e;
                         if (hit2) {
-                            r = r2;
+                            h0 = h1;
                             hit = true;
                         }
                     }
                 }
                 if (!hit) continue;
-                m.deliver(s, r);
+                m.deliver(s, h0);
                 if (faker && !(m.FLAGS() & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
                     m.FLAGS() |= FL_FAKE_DONE;
@@ -785,14 +779,14 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
 #endif
             cu32 *gin = (cu32 *)a.in;
             cu32 *gcnt = (cu32 *)a.in_count;
-            sm_node<ONE, HB_SM_UREC != 0>(a, n, f, k, inst * nodes + local, inst, local,
+            sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local,
                     lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
                     lds + o_dok + (size_t)li * C,
                     [&](int s) {
                         const uint32_t c = gcnt[sm_in_block(a, ui, s)] & 0x7FFFFFFFu;
                         return c < a.max_out ? c : a.max_out;
                     },
-                    [&](int s) { return (const uint32_t *)(gin + sm_in_block(a, ui, s) * MR); });
+                    [&](int s) { return gin + sm_in_block(a, ui, s) * MR; });
         } else {
             const uint32_t *cb = lcnt + (size_t)li * n;
             const uint32_t *rb = lrec + (size_t)li * n * MR;

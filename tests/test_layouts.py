@@ -307,8 +307,9 @@ def test_rebuilt_row_list_lengths(torch_cuda, count, n_erase):
     the balanced list kernel (leaf_hash_list_mix_kernel, kernels.hip) below
     2^18 listed rows of the worst case.  The list lengths here take each of its
     branches per CU share: pair-lane only (<= 128), one-lane only (129..256),
-    one round plus a pair-lane remainder, two and four one-lane rounds.  The
-    decode tree must come out as the proposer's tree."""
+    one round plus a pair-lane remainder (<= 384), and the long-list form
+    (> 384 per CU: one-lane rounds of 512 on all eight waves, ~490 and ~980
+    per CU here).  The decode tree must come out as the proposer's tree."""
     torch = torch_cuda
     n, f, plen = 64, 21, 2000
     rb = hb.RbcBatch(n, f, device=0)

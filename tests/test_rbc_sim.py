@@ -279,7 +279,10 @@ def _single_root_case(n):
 # kernel at 4 waves/SIMD (128 VGPRs, spills) and at the default budget, and the
 # global form; max_out 8 keeps the N=128 staged image under 64 KiB
 SM_FORMS = {"staged_w4": {"HBRBC_SM_W4": "1"}, "staged_w3": {"HBRBC_SM_W4": "0"},
-            "global": {"HBRBC_SM_STAGED": "0"}}
+            "global": {"HBRBC_SM_STAGED": "0"},
+            # the global-records kernel forced on (n = 64: two instances per
+            # block, one per wave) and off (n = 128: the staged records)
+            "grec_on": {"HBRBC_SM_GREC": "1"}, "grec_off": {"HBRBC_SM_GREC": "0"}}
 
 
 def test_single_root_scenarios_on_host():
