@@ -567,13 +567,56 @@ struct SmLayout {
     }
 };
 
+// The inbox of one instance, walked sender by sender in order: sender s's
+// record count and records sit at index idx(s) = ((s / R) * count + inst) * R
+// + s % R of the all-gathered inbox (sm_in_block), or at s in a staged LDS
+// copy (R = 0: no blocks).  The index moves incrementally -- +1, and (count
+// - 1) * R more after the last sender of a rank's block -- instead of the
+// per-sender 32-bit division and 64-bit products of sm_in_block, which the
+// ISA showed as ~50 scalar instructions per sender ahead of every record
+// read (round 5: the inbox loop was bound by the CU's scalar unit,
+// profiles/r5e_sm_counters.txt).  P: the pointer type (the global-records
+// kernel keeps the constant address space).
+template <class P>
+struct SmInbox {
+    P cnt, rec;        // counts [idx], records [idx][MR]
+    size_t idx, jump;  // jump: (count - 1) * R
+    uint32_t rr, R, MR, max_out;
+    __device__ __forceinline__ uint32_t count() const {
+        const uint32_t c = cnt[idx] & 0x7FFFFFFFu;
+        return c < max_out ? c : max_out;
+    }
+    __device__ __forceinline__ P recs() const { return rec + idx * MR; }
+    __device__ __forceinline__ void advance() {
+        ++idx;
+        if (R && ++rr == R) {
+            rr = 0;
+            idx += jump;
+        }
+    }
+};
+template <class P>
+__device__ __forceinline__ SmInbox<P> sm_inbox(P cnt, P rec, size_t inst, size_t count, uint32_t R,
+                                               uint32_t MR, uint32_t max_out) {
+    SmInbox<P> b;
+    b.cnt = cnt;
+    b.rec = rec;
+    b.idx = R ? inst * R : 0;   // sender 0: block 0, row 0
+    b.jump = R ? (count - 1) * R : 0;
+    b.rr = 0;
+    b.R = R;
+    b.MR = MR;
+    b.max_out = max_out;
+    return b;
+}
+
 // Handles one node's inbox of the round (or, in round 0, the proposer's
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
-// `inc(s)` sender s's record count, `recs(s)` its records.
-template <bool ONE, class InCount, class Recs>
+// `in` the instance's inbox at sender 0.
+template <bool ONE, class Inbox>
 __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
-                        InCount inc, Recs recs) {
+                        Inbox in) {
     const int me = (int)a.node_lo + local;
     const int W = (n + 31) / 32, C = (int)a.roots;
     const size_t sd = a.nodes;
@@ -624,11 +667,13 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         // keeps its address space: see HB_SM_CONSTAS)
         const int mw = me >> 5;
         auto rbit = [&](auto r) -> bool { return (r[1 + mw] >> (me & 31)) & 1u; };
-        for (int s = 0; s < n; ++s) {
+        // (no lane test for s == me: no record targets its own sender, so
+        // that lane's bit is clear -- a divergent `continue` cost exec-mask
+        // work on every sender)
+        for (int s = 0; s < n; ++s, in.advance()) {
             if (HB_SM_CACHE) m.em_focus(s >> 5);
-            if (s == me) continue;   // targets never include the sender
-            const uint32_t cnt = inc(s);
-            const auto rs = recs(s);
+            const uint32_t cnt = in.count();
+            const auto rs = in.recs();
             for (uint32_t e = 0; e < cnt; ++e) {
                 auto r = rs + (size_t)e * (1 + W);
                 uint32_t h0 = r[0];
@@ -700,11 +745,8 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     uint8_t *st = a.state + inst * a.nodes * sm_state_bytes(n, a.roots);
     sm_node<ONE>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
             a.decode_ok + inst * a.roots,
-            [&](int s) {
-                const uint32_t c = a.in_count[sm_in_block(a, inst, s)] & 0x7FFFFFFFu;
-                return c < a.max_out ? c : a.max_out;
-            },
-            [&](int s) { return a.in + sm_in_block(a, inst, s) * MR; });
+            sm_inbox<const uint32_t *>(a.in_count, a.in, inst, a.count, a.rows_per_rank,
+                                       (uint32_t)MR, a.max_out));
 }
 
 // Round kernel, staged form: a workgroup owns `ipb` whole instances (ipb x
@@ -782,17 +824,14 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
             sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local,
                     lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
                     lds + o_dok + (size_t)li * C,
-                    [&](int s) {
-                        const uint32_t c = gcnt[sm_in_block(a, ui, s)] & 0x7FFFFFFFu;
-                        return c < a.max_out ? c : a.max_out;
-                    },
-                    [&](int s) { return gin + sm_in_block(a, ui, s) * MR; });
+                    sm_inbox<cu32 *>(gcnt, gin, ui, a.count, a.rows_per_rank, (uint32_t)MR,
+                                     a.max_out));
         } else {
             const uint32_t *cb = lcnt + (size_t)li * n;
             const uint32_t *rb = lrec + (size_t)li * n * MR;
             sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
                     lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
-                    [&](int s) { return cb[s]; }, [&](int s) { return rb + (size_t)s * MR; });
+                    sm_inbox<const uint32_t *>(cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
         }
     }
     __syncthreads();
