@@ -261,11 +261,29 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
                   "ops_per_perm": opp, "ops_per_perm_source": src,
                   "measured_ceiling_perms_per_s": KECCAK_CEILING_PERMS,
                   "frac_of_measured_ceiling": pps / KECCAK_CEILING_PERMS,
+                  "sustained_clock": sustained_clock(dom, pps),
                   "profiled": profiled_frac(config, perms[dom], opp, per_launch)})
     else:
         r.update({"bound": "hbm", "achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                   "frac": hbm_gbs / HBM_PEAK_GBS})
     return r
+
+
+def sustained_clock(kernel, pps):
+    """The Keccak ceiling scaled to the clock the sponge kernels hold inside
+    the pipeline (profiles/effective_clock.json: GRBM_GUI_ACTIVE per dispatch
+    over its duration; the ceiling's register-only loop ran at 2.38 GHz, the
+    pipeline's sponges at 2.17): how close this kernel is to what the
+    power-managed clock allows.  None without the committed record."""
+    try:
+        c = json.load(open(os.path.join(ROOT, "profiles", "effective_clock.json")))
+        ghz = c["pipeline_ghz"]["leaf_hash_kernel" if kernel == "leaf_hash" else "validate_kernel"]
+        ceil = c["keccak_ceiling_perms_per_s_4_waves"] * ghz / c["keccak_ceiling_loop_ghz"]
+    except (OSError, ValueError, KeyError):
+        return None
+    return {"kernel_ghz": ghz, "ceiling_loop_ghz": c["keccak_ceiling_loop_ghz"],
+            "ceiling_perms_per_s_at_kernel_clock": ceil, "frac": pps / ceil,
+            "source": "profiles/effective_clock.json"}
 
 
 def profiled_frac(config, perms_per_launch, opp, per_launch):

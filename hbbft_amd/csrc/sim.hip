@@ -53,6 +53,12 @@
 #ifndef HB_SM_MERGE
 #define HB_SM_MERGE 1
 #endif
+// HB_SM_SELECT: the one-root Echo / EchoHash handler as predicated selects
+// (handle_echo_sel; round 5, default: sm_bench N=64 0.649-0.662 -> 0.625-0.630
+// ms, N=128 1.011-1.022 -> 0.993-1.001 ms, profiles/r5i_sm_select_ab.jsonl)
+#ifndef HB_SM_SELECT
+#define HB_SM_SELECT 1
+#endif
 // Global-records kernel: HB_SM_CONSTAS reads the inbox through the constant
 // address space, so the wave-uniform reads (counts, record headers) are
 // scalar loads; the recipient-mask word is per lane (a wave holds nodes of
@@ -387,6 +393,12 @@ struct Sm {
     // nodes, EchoHash for the right ones) runs the common part once.
     __device__ __forceinline__ void handle_echo_any(int s, uint32_t c, uint32_t j, uint32_t t,
                                                     bool full) {
+#if HB_SM_SELECT
+        if constexpr (ONE) {
+            handle_echo_sel(s, c, j, t, full);
+            return;
+        }
+#endif
         const uint32_t e = ECHO(s);
         int fk = -1;
         bool stop = false;
@@ -423,6 +435,54 @@ struct Sm {
         } else if (!full || (FLAGS() & FL_READY_SENT)) {
             compute_output(c);
         }
+    }
+    // The same handler with its common path as straight-line predicated
+    // work (one root): every check and counter update is a select, the mask
+    // word is read and written once, and only the rare steps -- a fault, the
+    // CanDecode and Ready sends, an output -- stay behind branches (each one
+    // guarded by a wave-wide test, so a wave in which no lane takes it skips
+    // it with one scalar branch).  Same order of effects as handle_echo_any:
+    // fault, entry and counters, CanDecode, Ready, compute_output.
+    __device__ __forceinline__ void handle_echo_sel(int s, uint32_t c, uint32_t j, uint32_t t,
+                                                    bool full) {
+        const int w = s >> 5;
+        const uint32_t b = 1u << (s & 31);
+        uint4 m4 = em_get(w);
+        const bool eh = m4.x & b, ef = m4.y & b, et = m4.z & b;   // entry: hash / full / tampered
+        const bool any = eh || ef;
+        // handle_echo (266-320): a stored full Echo of the same proof is a
+        // no-op, another one a MultipleEchos; a hash of another root too; a
+        // proof that does not validate an InvalidProof
+        const bool same_full = ef && !(et ^ (t & 1u)) && c == 0u && (int)j == s;
+        const bool bad_hash = eh && !ef && c != 0u;   // (one root: root_of(e) == 0)
+        bool stop, flt;
+        int fk;
+        if (full) {
+            const bool vp = validate_proof(c, j, t, s);
+            stop = ef || bad_hash || !vp;
+            flt = (ef && !same_full) || bad_hash || (!ef && !bad_hash && !vp);
+            fk = (ef || bad_hash) ? F_MULTIPLE_ECHOS : F_INVALID_PROOF;
+        } else {   // handle_echo_hash (322-355)
+            stop = any;
+            flt = any && c != 0u;
+            fk = F_MULTIPLE_ECHO_HASHES;
+        }
+        if (__builtin_expect(flt, 0)) fault(s, fk);
+        const bool go = !stop;
+        r_ce += (go && !any) ? 1 : 0;
+        r_cf += (go && full) ? 1 : 0;
+        // the entry: full (with its tamper bit) or hash
+        const uint32_t gb = go ? b : 0u;
+        m4.x = full ? (m4.x & ~gb) : (m4.x | gb);
+        m4.y = full ? (m4.y | gb) : m4.y;
+        m4.z = (full && (t & 1u)) ? (m4.z | gb) : m4.z;
+        em_put(w, m4);
+        const bool cd = go && full && !(r_flags & (1u << FL_CAN_DECODE_SHIFT)) && r_cf >= (uint32_t)k;
+        const bool rd_ok = go && !(r_flags & FL_READY_SENT) && r_ce >= (uint32_t)(n - f);
+        const bool co = go && (rd_ok ? full : (!full || (r_flags & FL_READY_SENT)));
+        if (__builtin_expect(cd, 0)) send_can_decode(c);
+        if (__builtin_expect(rd_ok, 0)) send_ready(c);
+        if (co) compute_output(c);
     }
     __device__ __forceinline__ void handle_echo(int s, uint32_t c, uint32_t j, uint32_t t) {
         handle_echo_any(s, c, j, t, true);
