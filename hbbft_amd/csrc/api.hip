@@ -240,7 +240,7 @@ struct hbrbc_ctx {
     int device = 0;
     size_t k = 0, m = 0, n = 0;
     int rt_enc = 2, rt_rec = 2;  // GF row tiles (rows per pass) for encode / reconstruct
-    int gf_mode = 0;             // generic kernel: 0 branch per bit, 1 hinted, 2 masked, 3 bit pairs, 4 input pairs, 5 coefficient switch
+    int gf_mode = 0;             // generic kernel: 0 branch per bit, 1 hinted, 2 masked, 3 bit pairs, 4 input pairs
     std::vector<uint8_t> matrix;  // n x k
     hipStream_t stream = nullptr;
     // specialised XOR-network modules (jit.hip): one module per output-row group
@@ -1186,7 +1186,6 @@ int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc
         else if (!std::strcmp(e, "bitslice_mask")) c->gf_mode = 2;
         else if (!std::strcmp(e, "bitslice_pair")) c->gf_mode = 3;
         else if (!std::strcmp(e, "bitslice_x2")) c->gf_mode = 4;
-        else if (!std::strcmp(e, "switch")) c->gf_mode = 5;
         else c->gf_mode = 0;
     }
     if (const char *e = getenv("HBRBC_RT_ENC")) c->rt_enc = std::max(2, std::min(16, atoi(e) & ~1));

@@ -584,184 +584,6 @@ __global__ __launch_bounds__(256) HB_GF_ATTR void gf_bitslice_kernel(
     }
 }
 
-// ------------------------------------------- GF product by a coefficient --
-// The generic reconstruct with the coefficient as a jump target instead of
-// eight bit tests.  c * x is linear over GF(2): output plane q of the
-// bit-sliced product is the XOR of the input planes p with bit q of c * 2^p
-// set -- a fixed network for each of the 256 coefficient values, ~4 planes
-// per output plane, i.e. ~16 v_xor3 per coefficient and 32 positions
-// (against ~32 v_xor + 3 doubling XORs + 16 scalar tests and branches in
-// gf_bitslice_kernel).  `gf_mulacc_dispatch` switches on the (wave-uniform,
-// scalar) coefficient into the network of its value; the 256 networks are
-// expanded at compile time from the field's multiplication table.
-constexpr uint32_t gfmul_ce(uint32_t a, uint32_t b) {
-    uint32_t r = 0;
-    for (int i = 0; i < 8; ++i) {
-        if (b & 1u) r ^= a;
-        b >>= 1;
-        a = (a & 0x80u) ? ((a << 1) ^ 0x11Du) : (a << 1);   // rse galois_8: poly 0x11D
-    }
-    return r & 0xFFu;
-}
-// input planes p of output plane q of c * x (bit q of c * 2^p)
-template <uint32_t C, int Q>
-constexpr uint32_t gf_plane_mask() {
-    uint32_t m = 0;
-    for (int p = 0; p < 8; ++p)
-        if ((gfmul_ce(C, 1u << p) >> Q) & 1u) m |= 1u << p;
-    return m;
-}
-// r ^ x[p] for every p in M, two planes per v_bitop3 (xor3): the plain XOR
-// chain was emitted as 2-input v_xor (~25 per coefficient), this is
-// sum over planes of ceil(|M| / 2) (~18)
-template <uint32_t M>
-__device__ __forceinline__ uint32_t gf_fold(uint32_t r, const uint32_t (&x)[8]) {
-    if constexpr (M == 0) {
-        return r;
-    } else {
-        constexpr int p1 = __builtin_ctz(M);
-        constexpr uint32_t M1 = M & (M - 1);
-        if constexpr (M1 == 0) {
-            return r ^ x[p1];
-        } else {
-            constexpr int p2 = __builtin_ctz(M1);
-            return gf_fold<M1 & (M1 - 1)>(__builtin_amdgcn_bitop3_b32(r, x[p1], x[p2], 0x96), x);
-        }
-    }
-}
-template <uint32_t C>
-__device__ __forceinline__ void gf_mulacc(uint32_t (&a)[8], const uint32_t (&x)[8]) {
-    a[0] = gf_fold<gf_plane_mask<C, 0>()>(a[0], x);
-    a[1] = gf_fold<gf_plane_mask<C, 1>()>(a[1], x);
-    a[2] = gf_fold<gf_plane_mask<C, 2>()>(a[2], x);
-    a[3] = gf_fold<gf_plane_mask<C, 3>()>(a[3], x);
-    a[4] = gf_fold<gf_plane_mask<C, 4>()>(a[4], x);
-    a[5] = gf_fold<gf_plane_mask<C, 5>()>(a[5], x);
-    a[6] = gf_fold<gf_plane_mask<C, 6>()>(a[6], x);
-    a[7] = gf_fold<gf_plane_mask<C, 7>()>(a[7], x);
-}
-__device__ __forceinline__ void gf_mulacc_dispatch(uint32_t c, uint32_t (&a)[8],
-                                                   const uint32_t (&x)[8]) {
-    switch (c & 0xFFu) {
-#define HB_GC1(n) \
-    case (n):     \
-        gf_mulacc<(n)>(a, x); \
-        break;
-#define HB_GC4(n) HB_GC1(n) HB_GC1((n) + 1) HB_GC1((n) + 2) HB_GC1((n) + 3)
-#define HB_GC16(n) HB_GC4(n) HB_GC4((n) + 4) HB_GC4((n) + 8) HB_GC4((n) + 12)
-#define HB_GC64(n) HB_GC16(n) HB_GC16((n) + 16) HB_GC16((n) + 32) HB_GC16((n) + 48)
-        HB_GC64(1) HB_GC64(65) HB_GC64(129)
-        HB_GC16(193) HB_GC16(209) HB_GC16(225) HB_GC4(241) HB_GC4(245) HB_GC4(249)
-        HB_GC1(253) HB_GC1(254) HB_GC1(255)
-#undef HB_GC64
-#undef HB_GC16
-#undef HB_GC4
-#undef HB_GC1
-        default:   // 0: nothing to add
-            break;
-    }
-}
-
-// Workgroup = nw waves over the same 2048 positions of one instance (as
-// gf_bitslice_kernel).  Every input row is loaded and transposed ONCE per
-// workgroup into LDS ([input][half][lane] 16-byte slots, conflict-free), then
-// each wave takes whole output rows o = wave, wave + nw, ...: eight
-// accumulator planes, one pass over the inputs from LDS, one switch per
-// coefficient.  Coefficients come from the decode-matrix cache in its
-// [pass][nin][16] layout (rt rows per pass).  LDS: nin x 2 KB (nin <= 48).
-__global__ __launch_bounds__(256) void gf_switch_kernel(
-    uint8_t *__restrict__ base, size_t inst_stride, RowMap rows, uint32_t row_bytes,
-    const uint8_t *__restrict__ coefs, size_t coef_slot_stride, int rt,
-    const uint32_t *__restrict__ in_idx, size_t in_idx_stride,
-    const uint32_t *__restrict__ out_idx, size_t out_idx_stride,
-    const int *__restrict__ nout_arr, int nout_uniform, const int *__restrict__ pat,
-    const uint64_t *__restrict__ slot_hash, uint64_t skip_hash, int hash_slots, int nin,
-    uint32_t waves_per_row, uint8_t *__restrict__ uf_payload, size_t uf_stride, uint32_t uf_S,
-    uint32_t uf_k, const int32_t *__restrict__ uf_status) {
-    extern __shared__ uint4 gsw_lds[];
-    const size_t inst = blockIdx.x / waves_per_row;
-    const int slot = pat ? pat[inst] : (int)inst;
-    if (skip_hash && slot < hash_slots && slot_hash[slot] == skip_hash) return;
-    const int wave = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
-    const uint32_t wchunk = blockIdx.x - (uint32_t)inst * waves_per_row, lane = threadIdx.x & 63;
-    uint32_t off = wchunk * 2048 + lane * 16;
-    const bool active = off < row_bytes;
-    if (!active) off = row_bytes - 16;
-    const bool full = off + 1024 + 16 <= row_bytes;
-    const uint32_t d2 = full ? 1024 : 0;
-    uint8_t *ib = base + inst * inst_stride;
-    const int nout = nout_arr ? nout_arr[slot] : nout_uniform;
-    const uint8_t *cf = coefs + (size_t)slot * coef_slot_stride;
-    const uint32_t *iidx = in_idx + (size_t)slot * in_idx_stride;
-    const uint32_t *oidx = out_idx + (size_t)slot * out_idx_stride;
-    uint8_t *ufp = (uf_payload && uf_status[inst] == 0) ? uf_payload + inst * uf_stride : nullptr;
-    if (nout == 0) {
-        // nothing to rebuild: the data rows are rows 0..k-1 as they are
-        if (ufp && wave == 0 && active) {
-            for (uint32_t r = 0; r < uf_k; ++r) {
-                const uint8_t *src = ib + rows.off(r) + off;
-                const uint4 l = *reinterpret_cast<const uint4 *>(src);
-                unframe_put(ufp, uf_S, r, off, l.x, l.y, l.z, l.w);
-                if (full) {
-                    const uint4 h = *reinterpret_cast<const uint4 *>(src + d2);
-                    unframe_put(ufp, uf_S, r, off + d2, h.x, h.y, h.z, h.w);
-                }
-            }
-        }
-        return;   // uniform over the block
-    }
-    // stage: input j by wave j % nw, transposed into its 8 planes
-    for (int j = __builtin_amdgcn_readfirstlane(wave); j < nin; j += nw) {
-        const uint32_t r = iidx[j];
-        const uint8_t *src = ib + rows.off(r) + off;
-        const uint4 lo = *reinterpret_cast<const uint4 *>(src);
-        const uint4 hi = full ? *reinterpret_cast<const uint4 *>(src + d2) : make_uint4(0, 0, 0, 0);
-        if (ufp && r < uf_k && active) {   // present data rows: payload bytes as they are
-            unframe_put(ufp, uf_S, r, off, lo.x, lo.y, lo.z, lo.w);
-            if (full) unframe_put(ufp, uf_S, r, off + d2, hi.x, hi.y, hi.z, hi.w);
-        }
-        uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        bs_transpose(x);
-        gsw_lds[(j * 2 + 0) * 64 + lane] = make_uint4(x[0], x[1], x[2], x[3]);
-        gsw_lds[(j * 2 + 1) * 64 + lane] = make_uint4(x[4], x[5], x[6], x[7]);
-    }
-    // the slot's coefficients, [output][input] bytes (inputs padded to 4),
-    // behind the planes: four coefficients per LDS read in the loop below
-    const int nin4 = (nin + 3) & ~3;
-    uint8_t *lcoef = reinterpret_cast<uint8_t *>(gsw_lds + (size_t)nin * 2 * 64);
-    for (int i = threadIdx.x; i < nout * nin4; i += blockDim.x) {
-        const int o = i / nin4, j = i - o * nin4;
-        lcoef[i] = j < nin ? cf[((size_t)(o / rt) * nin + j) * 16 + (o % rt)] : 0;
-    }
-    __syncthreads();
-    const uint32_t *lc32 = reinterpret_cast<const uint32_t *>(lcoef);
-    for (int o = __builtin_amdgcn_readfirstlane(wave); o < nout; o += nw) {
-        uint32_t acc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-        for (int j4 = 0; j4 < nin; j4 += 4) {
-            const uint32_t c4 = rfl(lc32[(o * nin4 + j4) >> 2]);
-            const int jn = nin - j4 < 4 ? nin - j4 : 4;
-            for (int q = 0; q < jn; ++q) {
-                const int j = j4 + q;
-                const uint4 pa = gsw_lds[(j * 2 + 0) * 64 + lane];
-                const uint4 pb = gsw_lds[(j * 2 + 1) * 64 + lane];
-                const uint32_t x[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-                gf_mulacc_dispatch((c4 >> (8 * q)) & 0xFFu, acc, x);
-            }
-        }
-        if (active) {
-            bs_transpose(acc);
-            const uint32_t orow = oidx[o];
-            uint8_t *dst = ib + rows.off(orow) + off;
-            store16_stream(dst, acc[0], acc[1], acc[2], acc[3]);
-            if (full) store16_stream(dst + d2, acc[4], acc[5], acc[6], acc[7]);
-            if (ufp && orow < uf_k) {
-                unframe_put(ufp, uf_S, orow, off, acc[0], acc[1], acc[2], acc[3]);
-                if (full) unframe_put(ufp, uf_S, orow, off + d2, acc[4], acc[5], acc[6], acc[7]);
-            }
-        }
-    }
-}
-
 // ----------------------------------------------------------- leaf hashes --
 // One SHA3-256 sponge per lane: lane g hashes shard (g % n) of instance
 // (g / n).  All lanes share the shard length, so every branch is uniform.
@@ -1655,26 +1477,6 @@ hipError_t launch_gf_apply(const GfApplyArgs &a, hipStream_t s) {
     const size_t blocks = (size_t)wpr * a.count;
     if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const int max_rows = a.nout ? a.max_rows : a.nout_uniform;
-    if (a.mode == 5 && a.nin <= 48) {
-        // coefficient switch (gf_switch_kernel): whole output rows per wave,
-        // every input transposed once per workgroup into LDS
-        int nw = std::max(1, std::min(4, max_rows));
-        if (const char *we = getenv("HBRBC_GF_WAVES")) nw = std::max(1, std::min(4, atoi(we)));
-        // planes nin x 2 KB, then the coefficients [max_rows][nin rounded to 4]
-        const size_t lds = (size_t)a.nin * 2048 + (size_t)max_rows * ((a.nin + 3) & ~3);
-        static bool attr = false;
-        if (!attr && lds > 65536) {
-            hipFuncSetAttribute(reinterpret_cast<const void *>(gf_switch_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            attr = true;
-        }
-        hipLaunchKernelGGL(gf_switch_kernel, dim3((unsigned)blocks), dim3(64 * nw), lds, s, a.base,
-                           a.inst_stride, a.rows, row_bytes, a.coefs, a.coef_slot_stride, a.rt,
-                           a.in_idx, a.in_idx_stride, a.out_idx, a.out_idx_stride, a.nout,
-                           a.nout_uniform, a.pat, a.slot_hash, a.skip_hash, a.hash_slots, a.nin,
-                           wpr, a.payload, a.payload_stride, a.payload_S, a.payload_k, a.rstatus);
-        return hipGetLastError();
-    }
     // waves per block: the fewest that keep the longest wave at the minimum
     // number of passes (a wave beyond an instance's passes exits at once, but
     // its slot in the block idles a SIMD: cfg3, 42 rows at most in 7-row

@@ -332,14 +332,12 @@ def test_full_size_roundtrip_properties(torch_cuda):
         assert np.array_equal(r["nodes"][i], nd)
 
 
-@pytest.mark.parametrize("kind", ["bitslice", "bitslice_mask", "bitslice_pair", "bitslice_x2",
-                                  "switch"])
+@pytest.mark.parametrize("kind", ["bitslice", "bitslice_mask", "bitslice_pair", "bitslice_x2"])
 @pytest.mark.parametrize("k,m,L", [(22, 42, 11916), (6, 10, 4099), (84, 166, 61), (1, 3, 48),
                                    (13, 7, 33), (3, 2, 16)])
 def test_gf_kernel_variants_vs_oracle(torch_cuda, monkeypatch, kind, k, m, L):
     """Every generic GF kernel form (branch per coefficient bit, masked, bit
-    pairs, input pairs, coefficient switch -- which falls back to the
-    bit-sliced kernel above 48 inputs) is bit-exact,
+    pairs, input pairs) is bit-exact,
     including rows whose length is not a multiple of 32 (bit-sliced lanes own
     32 bytes) and worst-case erasures."""
     monkeypatch.setenv("HBRBC_GF", kind)

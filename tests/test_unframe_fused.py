@@ -46,10 +46,9 @@ def _decode(torch, rb, slab, S, present, roots, env):
 
 @pytest.mark.parametrize("n,plen", [(16, 2396), (16, 2380), (64, 262144), (7, 1000), (4, 8),
                                     (64, 16380), (31, 5000)])
-@pytest.mark.parametrize("gf", ["bitslice", "bitslice_x2", "switch"])
+@pytest.mark.parametrize("gf", ["bitslice", "bitslice_x2"])
 def test_fused_unframe_matches_separate_and_oracle(torch_cuda, monkeypatch, n, plen, gf):
-    """(gf: the generic reconstruct form, one input or input pairs per step,
-    or the coefficient switch)"""
+    """(gf: the generic reconstruct form, one input or input pairs per step)"""
     torch = torch_cuda
     import hbbft_amd as hb
     monkeypatch.setenv("HBRBC_GF", gf)

@@ -8,7 +8,7 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp HBRBC_JIT=load
 OUT=$ROOT/gpurun_out/r5e
 mkdir -p $OUT
 fatal() { case "$1" in 124|134|137|139) return 0;; esac; return 1; }
-timeout -k 10 600 python -u -m pytest tests/test_rbc_sim.py tests/test_layouts.py tests/test_drop_rows.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
+HBRBC_JIT= timeout -k 10 600 python -u -m pytest tests/test_rbc_sim.py tests/test_layouts.py tests/test_drop_rows.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; echo "tests exit $rc"; tail -2 $OUT/tests.log; if fatal $rc; then exit $rc; fi
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/sm_trace -o run -- python3 $ROOT/tools/sm_bench.py --reps 3 > $OUT/sm_trace.log 2>&1
 rc=$?; echo "sm trace exit $rc"; grep '^{' $OUT/sm_trace.log; if fatal $rc; then exit $rc; fi
