@@ -908,8 +908,11 @@ __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, i
 // for launches whose LDS image leaves room for more than 3 waves per SIMD
 // (N=64 validator-sharded object: state machine 0.82 -> 0.63 ms per step;
 // at N=128 the LDS holds 2 waves per SIMD and the spills cost 1.25 -> 1.28)
+#ifndef HB_SM_W4_WAVES
+#define HB_SM_W4_WAVES 4   // waves/SIMD of the "w4" forms (A/B: -DHB_SM_W4_WAVES=5)
+#endif
 template <bool ONE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_staged_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
     sm_round_staged<ONE>(a, n, f, k, ipb);
 }
@@ -919,7 +922,7 @@ __global__ __launch_bounds__(256) void sm_round_grec_kernel(hbrbc_sm_args a, int
     sm_round_staged<ONE, true>(a, n, f, k, ipb);
 }
 template <bool ONE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_grec_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
     sm_round_staged<ONE, true>(a, n, f, k, ipb);
 }
