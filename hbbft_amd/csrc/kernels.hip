@@ -1817,13 +1817,14 @@ __global__ __launch_bounds__(kBlock) void drop_rows_kernel(
     const size_t inst = blockIdx.x;
     for (uint32_t j = threadIdx.x; j < n; j += kBlock) pres[j] = present[inst * n + j];
     __syncthreads();
+    const uint4 v = make_uint4(fill, fill, fill, fill);
     uint8_t *ib = shards + inst * inst_stride;
     for (uint32_t j = 0; j < n; ++j) {
         if (pres[j]) continue;
-        uint8_t *row = ib + rows.off(j);
-        // streamed (non-temporal) like the other kernels' row outputs
-        for (uint32_t c = threadIdx.x; c < slot16; c += kBlock)
-            store16_stream(row + 16 * (size_t)c, fill, fill, fill, fill);
+        // plain stores: non-temporal ones measured slower here (cfg3 erase
+        // 1.81 -> 1.96 ms, profiles/r5d_bench.json vs r5k_cfg3_trace_bench.json)
+        uint4 *row = reinterpret_cast<uint4 *>(ib + rows.off(j));
+        for (uint32_t c = threadIdx.x; c < slot16; c += kBlock) row[c] = v;
     }
 }
 
