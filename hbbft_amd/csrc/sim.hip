@@ -71,12 +71,20 @@
 #ifndef HB_SM_CONSTAS
 #define HB_SM_CONSTAS 1
 #endif
+#ifndef HB_SM_PREFETCH
+#define HB_SM_PREFETCH 1
+#endif
 
 namespace hbrbc {
 
 namespace {
 
 constexpr uint32_t kNone = 0xFFu;
+// the inbox as global-address-space words (the prefetch's vector loads)
+typedef __attribute__((address_space(1))) const uint32_t gu32;
+__device__ __forceinline__ uint32_t rfl_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
 
 // message kinds (broadcast::Message, message.rs:13-24) + the fake block
 enum { K_VALUE = 0, K_ECHO = 1, K_READY = 2, K_CAN_DECODE = 3, K_ECHO_HASH = 4, K_FAKE = 5 };
@@ -567,11 +575,28 @@ struct Sm {
         }
     }
 
-    // r: the record (a generic pointer, or a constant-address-space one whose
-    // wave-uniform reads are scalar loads); only its header word is read here
+    // h0: the record's header word.  LEAN: the rounds >= 2 of a batch without
+    // injected broadcasts, whose inboxes hold only Echo / EchoHash / Ready /
+    // CanDecode records (Values go out in round 0 only, Fake records only from
+    // a fake_from node): the Value and Fake handlers are not compiled in, and a
+    // record of those kinds sets `bad` (the launch reports it, emitted[1] bit 1).
+    bool bad = false;
+    template <bool LEAN>
     __device__ __forceinline__ void deliver(int s, uint32_t h0) {
         const uint32_t kind = h0 & 0xFFu, c0 = (h0 >> 8) & 0xFFu;
         const uint32_t j = (h0 >> 16) & 0xFFu, t = (h0 >> 24) & 0xFFu;
+        if constexpr (LEAN) {
+            switch (kind) {
+                case K_ECHO:
+                case K_ECHO_HASH: handle_echo_any(s, c0, j, t, kind == K_ECHO); break;
+                case K_READY: handle_ready_core(s, c0, true); break;
+                case K_CAN_DECODE: handle_can_decode(s, c0); break;
+                case K_VALUE:
+                case K_FAKE: bad = true; break;
+                default: break;
+            }
+            return;
+        }
         switch (kind) {
             case K_VALUE: {
                 // the proposer's Value to us: proof (value_root[me], me, value_tamper[me]);
@@ -637,16 +662,20 @@ struct SmLayout {
 // read (round 5: the inbox loop was bound by the CU's scalar unit,
 // profiles/r5e_sm_counters.txt).  P: the pointer type (the global-records
 // kernel keeps the constant address space).
-template <class P>
+template <class P, class Q>
 struct SmInbox {
     P cnt, rec;        // counts [idx], records [idx][MR]
+    Q vcnt, vrec;      // the same through the prefetch's pointer type
     size_t idx, jump;  // jump: (count - 1) * R
     uint32_t rr, R, MR, max_out;
-    __device__ __forceinline__ uint32_t count() const {
-        const uint32_t c = cnt[idx] & 0x7FFFFFFFu;
+    __device__ __forceinline__ uint32_t clamp(uint32_t c) const {
+        c &= 0x7FFFFFFFu;
         return c < max_out ? c : max_out;
     }
+    __device__ __forceinline__ uint32_t count() const { return clamp(cnt[idx]); }
     __device__ __forceinline__ P recs() const { return rec + idx * MR; }
+    __device__ __forceinline__ uint32_t vcount_raw() const { return vcnt[idx]; }
+    __device__ __forceinline__ Q vrecs() const { return vrec + idx * MR; }
     __device__ __forceinline__ void advance() {
         ++idx;
         if (R && ++rr == R) {
@@ -655,12 +684,15 @@ struct SmInbox {
         }
     }
 };
-template <class P>
-__device__ __forceinline__ SmInbox<P> sm_inbox(P cnt, P rec, size_t inst, size_t count, uint32_t R,
-                                               uint32_t MR, uint32_t max_out) {
-    SmInbox<P> b;
+template <class P, class Q>
+__device__ __forceinline__ SmInbox<P, Q> sm_inbox(P cnt, P rec, Q vcnt, Q vrec, size_t inst,
+                                                  size_t count, uint32_t R, uint32_t MR,
+                                                  uint32_t max_out) {
+    SmInbox<P, Q> b;
     b.cnt = cnt;
     b.rec = rec;
+    b.vcnt = vcnt;
+    b.vrec = vrec;
     b.idx = R ? inst * R : 0;   // sender 0: block 0, row 0
     b.jump = R ? (count - 1) * R : 0;
     b.rr = 0;
@@ -673,7 +705,7 @@ __device__ __forceinline__ SmInbox<P> sm_inbox(P cnt, P rec, size_t inst, size_t
 // Handles one node's inbox of the round (or, in round 0, the proposer's
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
 // `in` the instance's inbox at sender 0.
-template <bool ONE, class Inbox>
+template <bool ONE, bool LEAN, class Inbox>
 __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
                         Inbox in) {
@@ -707,7 +739,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     m.faults = a.faults + g * (size_t)a.max_faults;
     m.nfault = a.fault_count[g];
     m.cache_in();
-    if (a.round == 0) {
+    if (!LEAN && a.round == 0) {
         // the proposer's broadcast() (broadcast.rs:123-137, 170-225): its input
         // step goes out unfiltered (VirtualNet::send_input; only deliveries to
         // faulty nodes pass the adversary)
@@ -722,23 +754,64 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         }
     } else {
         m.drop = m.role == R_SILENT;
-        const bool faker = a.fake_from[inst] == (uint8_t)me;
-        // this node's bit in a record's recipient mask (the record pointer
+        const bool faker = !LEAN && a.fake_from[inst] == (uint8_t)me;
+        // this node's word of a record's recipient mask (the record pointer
         // keeps its address space: see HB_SM_CONSTAS)
         const int mw = me >> 5;
-        auto rbit = [&](auto r) -> bool { return (r[1 + mw] >> (me & 31)) & 1u; };
+        const uint32_t rw = 1 + W, mb = (uint32_t)(me & 31);
+        // HB_SM_PREFETCH: sender s + 1's count and the headers and mask words
+        // of its first two records are in flight while sender s is handled
+        // (vector loads: their waits do not drain the LDS counter the
+        // handlers' state accesses wait on)
+        const bool two = a.max_out >= 2;
+        uint32_t pc = 0, ph0 = 0, ph1 = 0, pm0 = 0, pm1 = 0;
+        auto fetch = [&]() {
+            const auto q = in.vrecs();
+            const auto q1 = q + (two ? rw : 0u);
+            pc = in.vcount_raw();
+            ph0 = q[0];
+            pm0 = q[1 + mw];
+            ph1 = q1[0];
+            pm1 = q1[1 + mw];
+        };
+        if (HB_SM_PREFETCH) fetch();
         // (no lane test for s == me: no record targets its own sender, so
         // that lane's bit is clear -- a divergent `continue` cost exec-mask
         // work on every sender)
-        for (int s = 0; s < n; ++s, in.advance()) {
+        for (int s = 0; s < n; ++s) {
             if (HB_SM_CACHE) m.em_focus(s >> 5);
-            const uint32_t cnt = in.count();
             const auto rs = in.recs();
+            uint32_t cnt, h0p = 0, h1p = 0, m0p = 0, m1p = 0;
+            if (HB_SM_PREFETCH) {
+                cnt = in.clamp(rfl_u(pc));
+                h0p = rfl_u(ph0);
+                h1p = rfl_u(ph1);
+                m0p = pm0;
+                m1p = pm1;
+                if (s + 1 < n) {
+                    in.advance();
+                    fetch();
+                }
+            } else {
+                cnt = in.count();
+                in.advance();
+            }
+            // header and this node's mask word of record e
+            auto get = [&](uint32_t e, uint32_t &h, uint32_t &mk) {
+                if (HB_SM_PREFETCH && e < 2) {
+                    h = e ? h1p : h0p;
+                    mk = e ? m1p : m0p;
+                } else {
+                    const auto r = rs + (size_t)e * rw;
+                    h = r[0];
+                    mk = r[1 + mw];
+                }
+            };
             for (uint32_t e = 0; e < cnt; ++e) {
-                auto r = rs + (size_t)e * (1 + W);
-                uint32_t h0 = r[0];
+                uint32_t h0, mk0;
+                get(e, h0, mk0);
                 const uint32_t k0 = h0 & 0xFFu;
-                bool hit = rbit(r);
+                bool hit = (mk0 >> mb) & 1u;
                 // An Echo and an EchoHash of the same sender in a row whose
                 // targets do not overlap at this node (handle_value emits
                 // Echo to all but the right nodes, EchoHash to the right
@@ -751,11 +824,11 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
                 if (HB_SM_MERGE) {
                     bool pair = false, hit2 = false;
                     uint32_t h1 = 0;
-                    const auto r2 = r + (1 + W);
                     if ((k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
-                        h1 = r2[0];
+                        uint32_t mk1;
+                        get(e + 1, h1, mk1);
                         const uint32_t k1 = h1 & 0xFFu;
-                        hit2 = rbit(r2);
+                        hit2 = (mk1 >> mb) & 1u;
                         pair = (k1 == K_ECHO || k1 == K_ECHO_HASH) && k1 != k0 && !(hit && hit2);
                     }
                     if (__all(pair)) {
@@ -767,7 +840,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
                     }
                 }
                 if (!hit) continue;
-                m.deliver(s, h0);
+                m.template deliver<LEAN>(s, h0);
                 if (faker && !(m.FLAGS() & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
                     m.FLAGS() |= FL_FAKE_DONE;
@@ -783,6 +856,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     a.fault_count[g] = m.nfault;
     if (m.nout) atomicAdd(a.emitted, m.nout);
     if (m.overflow) atomicOr(a.emitted + 1, 1u);
+    if (LEAN && m.bad) atomicOr(a.emitted + 1, 2u);
 }
 
 __device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t inst, int s) {
@@ -793,7 +867,7 @@ __device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t ins
 // Round kernel, global form: one thread per (instance, hosted node), state,
 // records and outcomes read where they lie.  For blocks whose staged copy
 // does not fit the LDS budget (sm_plan).
-template <bool ONE>
+template <bool ONE, bool LEAN>
 __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, int f, int k) {
     if (a.active && *a.active == 0u) return;   // quiescent: nothing was sent last round
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -803,10 +877,10 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     if ((int)a.node_lo + local >= n) return;
     const size_t MR = (size_t)a.max_out * ((n + 31) / 32 + 1);
     uint8_t *st = a.state + inst * a.nodes * sm_state_bytes(n, a.roots);
-    sm_node<ONE>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
+    sm_node<ONE, LEAN>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
             a.decode_ok + inst * a.roots,
-            sm_inbox<const uint32_t *>(a.in_count, a.in, inst, a.count, a.rows_per_rank,
-                                       (uint32_t)MR, a.max_out));
+            sm_inbox(a.in_count, a.in, (gu32 *)a.in_count, (gu32 *)a.in, inst, a.count,
+                     a.rows_per_rank, (uint32_t)MR, a.max_out));
 }
 
 // Round kernel, staged form: a workgroup owns `ipb` whole instances (ipb x
@@ -824,7 +898,7 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
 // KB per instance), so the grid's blocks fit the chip in one round instead of
 // 1.3 (a second, mostly idle round of blocks), and the per-thread staging
 // loop over the records (a chain of dependent global loads) goes away.
-template <bool ONE, bool GREC = false>
+template <bool ONE, bool GREC, bool LEAN>
 __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, int f, int k,
                                                 int ipb) {
     extern __shared__ uint4 sm_lds4[];
@@ -881,17 +955,17 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
 #endif
             cu32 *gin = (cu32 *)a.in;
             cu32 *gcnt = (cu32 *)a.in_count;
-            sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local,
+            sm_node<ONE, LEAN>(a, n, f, k, inst * nodes + local, inst, local,
                     lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
                     lds + o_dok + (size_t)li * C,
-                    sm_inbox<cu32 *>(gcnt, gin, ui, a.count, a.rows_per_rank, (uint32_t)MR,
-                                     a.max_out));
+                    sm_inbox(gcnt, gin, (gu32 *)a.in_count, (gu32 *)a.in, ui, a.count,
+                             a.rows_per_rank, (uint32_t)MR, a.max_out));
         } else {
             const uint32_t *cb = lcnt + (size_t)li * n;
             const uint32_t *rb = lrec + (size_t)li * n * MR;
-            sm_node<ONE>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
+            sm_node<ONE, LEAN>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
                     lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
-                    sm_inbox<const uint32_t *>(cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
+                    sm_inbox(cb, rb, cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
         }
     }
     __syncthreads();
@@ -899,10 +973,10 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
         reinterpret_cast<uint2 *>(gst)[i] = reinterpret_cast<const uint2 *>(lds)[i];
 }
 
-template <bool ONE>
+template <bool ONE, bool LEAN>
 __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
                                                               int k, int ipb) {
-    sm_round_staged<ONE>(a, n, f, k, ipb);
+    sm_round_staged<ONE, false, LEAN>(a, n, f, k, ipb);
 }
 // The same at 4 waves/SIMD (128 VGPRs, a few spills instead of 162 VGPRs):
 // for launches whose LDS image leaves room for more than 3 waves per SIMD
@@ -911,20 +985,20 @@ __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, i
 #ifndef HB_SM_W4_WAVES
 #define HB_SM_W4_WAVES 4   // waves/SIMD of the "w4" forms (A/B: -DHB_SM_W4_WAVES=5)
 #endif
-template <bool ONE>
+template <bool ONE, bool LEAN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_staged_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
-    sm_round_staged<ONE>(a, n, f, k, ipb);
+    sm_round_staged<ONE, false, LEAN>(a, n, f, k, ipb);
 }
-template <bool ONE>
+template <bool ONE, bool LEAN>
 __global__ __launch_bounds__(256) void sm_round_grec_kernel(hbrbc_sm_args a, int n, int f, int k,
                                                             int ipb) {
-    sm_round_staged<ONE, true>(a, n, f, k, ipb);
+    sm_round_staged<ONE, true, LEAN>(a, n, f, k, ipb);
 }
-template <bool ONE>
+template <bool ONE, bool LEAN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_grec_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
-    sm_round_staged<ONE, true>(a, n, f, k, ipb);
+    sm_round_staged<ONE, true, LEAN>(a, n, f, k, ipb);
 }
 
 }  // namespace
@@ -940,9 +1014,10 @@ static size_t sm_lds_bytes(const hbrbc_sm_args &a, int n, int ipb, bool grec = f
     return ((size_t)ipb * per + 15) & ~(size_t)15;
 }
 
-hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s) {
+// One instantiation set per handler set (LEAN: see Sm::deliver).
+template <bool LEAN>
+static hipError_t launch_sm_form(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s) {
     const size_t threads = a.count * a.nodes;
-    if (threads == 0) return hipSuccess;
     const char *e = getenv("HBRBC_SM_STAGED");   // 0: the global form (A/B)
     const bool staged_ok = !(e && !strcmp(e, "0")) && a.nodes <= 256;
     int ipb = a.nodes >= 128 ? 1 : (int)(128 / a.nodes);
@@ -963,19 +1038,32 @@ hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStrea
         const char *w4e = getenv("HBRBC_SM_W4");
         const bool w4 = w4e ? !strcmp(w4e, "1")
                             : (163840 / lds) * ((threads_pb + 63) / 64) > 12;
-        auto kern = grec ? (a.roots == 1 ? (w4 ? sm_round_grec_w4_kernel<true> : sm_round_grec_kernel<true>)
-                                         : (w4 ? sm_round_grec_w4_kernel<false> : sm_round_grec_kernel<false>))
-                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true> : sm_round_staged_kernel<true>)
-                                         : (w4 ? sm_round_staged_w4_kernel<false> : sm_round_staged_kernel<false>));
+        auto kern = grec ? (a.roots == 1 ? (w4 ? sm_round_grec_w4_kernel<true, LEAN>
+                                               : sm_round_grec_kernel<true, LEAN>)
+                                         : (w4 ? sm_round_grec_w4_kernel<false, LEAN>
+                                               : sm_round_grec_kernel<false, LEAN>))
+                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true, LEAN>
+                                               : sm_round_staged_kernel<true, LEAN>)
+                                         : (w4 ? sm_round_staged_w4_kernel<false, LEAN>
+                                               : sm_round_staged_kernel<false, LEAN>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3((unsigned)threads_pb), lds, s, a, n, f, k, ipb);
         return hipGetLastError();
     }
     const unsigned blocks = (unsigned)((threads + 255) / 256);
     if (a.roots == 1)
-        hipLaunchKernelGGL(sm_round_kernel<true>, dim3(blocks), dim3(256), 0, s, a, n, f, k);
+        hipLaunchKernelGGL((sm_round_kernel<true, LEAN>), dim3(blocks), dim3(256), 0, s, a, n, f, k);
     else
-        hipLaunchKernelGGL(sm_round_kernel<false>, dim3(blocks), dim3(256), 0, s, a, n, f, k);
+        hipLaunchKernelGGL((sm_round_kernel<false, LEAN>), dim3(blocks), dim3(256), 0, s, a, n, f, k);
     return hipGetLastError();
+}
+
+hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s) {
+    if (a.count * a.nodes == 0) return hipSuccess;
+    // the lean handler set for rounds >= 2 of a batch the caller marks as
+    // having no injected broadcasts (HBRBC_SM_LEAN=0: never, A/B)
+    const char *le = getenv("HBRBC_SM_LEAN");
+    const bool lean = (a.flags & HBRBC_SM_NO_FAKE) && a.round >= 2 && !(le && !strcmp(le, "0"));
+    return lean ? launch_sm_form<true>(a, n, f, k, s) : launch_sm_form<false>(a, n, f, k, s);
 }
 
 }  // namespace hbrbc

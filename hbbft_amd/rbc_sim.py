@@ -56,7 +56,11 @@ class SmArgs(ctypes.Structure):
         (name, _P) for name in (
             "proposer", "role", "value_root", "value_tamper", "proof_ok", "decode_ok",
             "fake_from", "fake_root", "fake_list", "in_", "in_count", "out", "out_count",
-            "state", "output_root", "faults", "fault_count", "emitted", "active")]
+            "state", "output_root", "faults", "fault_count", "emitted", "active")] + [
+        ("flags", ctypes.c_uint32)]
+
+
+SM_NO_FAKE = 1   # hbrbc_sm_args.flags: no instance injects broadcasts (HBRBC_SM_NO_FAKE)
 
 
 def sm_state_bytes_host(n, roots):
@@ -227,6 +231,9 @@ class StateMachineRank:
         sb = L.hbrbc_sm_state_bytes(n, roots)
         R, cnt = self.R, count
         self.sc = sc
+        # no fake_from node anywhere: rounds >= 2 run the kernels without the
+        # Value / Fake handlers (sim.hip Sm::deliver, LEAN)
+        self.flags = SM_NO_FAKE if bool((sc["fake_from"] == NONE).all()) else 0
         self.ok, self.dec = ok, dec
         self.state = torch.zeros((cnt, R, sb), dtype=torch.uint8, device=dev)
         self.out = torch.zeros((cnt, R, max_out, self.rec), dtype=torch.int32, device=dev)
@@ -273,7 +280,8 @@ class StateMachineRank:
             raise RuntimeError("state machine: round %d past max_rounds %d" % (r, self.max_rounds))
         s = self.sc
         a = SmArgs(count=self.count, node_lo=self.node_lo, nodes=self.R, rows_per_rank=self.R,
-                   roots=self.roots, max_out=self.max_out, max_faults=self.max_faults, round=r)
+                   roots=self.roots, max_out=self.max_out, max_faults=self.max_faults, round=r,
+                   flags=self.flags)
         for name in ("proposer", "role", "value_root", "value_tamper", "fake_from", "fake_root",
                      "fake_list"):
             setattr(a, name, s[name].data_ptr())
@@ -343,7 +351,11 @@ def _check_batch(ranks, h, r0, own=None):
     quiescent (no records anywhere), else None.  own: the records of THIS
     rank per (sub-batch, round) where h holds every rank's totals."""
     for i in range(h.shape[1]):
-        if int(h[:, i, 1].max()):
+        fl = int(h[:, i, 1].max())
+        if fl & 2:
+            raise RuntimeError("state machine: a Value or Fake record reached a round run "
+                               "without those handlers (hbrbc_sm_args.flags)")
+        if fl:
             raise RuntimeError("state machine: a node emitted more than %d messages in a round"
                                % ranks[0].max_out)
         mine = h[:, i, 0] if own is None else own[:, i]

@@ -524,7 +524,13 @@ typedef struct hbrbc_sm_args {
                                      (every sender's previous round emitted nothing: the
                                      network is quiescent), so a host can enqueue several
                                      rounds and read the emitted counts back once */
+    uint32_t flags;               /* HBRBC_SM_NO_FAKE: no instance has a fake_from node, so the
+                                     inboxes of rounds >= 2 hold only Echo, EchoHash, Ready and
+                                     CanDecode records and those rounds run a kernel without the
+                                     Value / Fake handlers (a record of another kind there sets
+                                     emitted[1] bit 1, the caller's error) */
 } hbrbc_sm_args;
+#define HBRBC_SM_NO_FAKE 1u
 size_t hbrbc_sm_state_bytes(size_t n, size_t roots);
 /* One round for the hosted nodes of every instance (ctx gives n, f, k). */
 int hbrbc_sm_round(hbrbc_ctx *ctx, const hbrbc_sm_args *args, void *stream);

@@ -282,7 +282,10 @@ SM_FORMS = {"staged_w4": {"HBRBC_SM_W4": "1"}, "staged_w3": {"HBRBC_SM_W4": "0"}
             "global": {"HBRBC_SM_STAGED": "0"},
             # the global-records kernel forced on (n = 64: two instances per
             # block, one per wave) and off (n = 128: the staged records)
-            "grec_on": {"HBRBC_SM_GREC": "1"}, "grec_off": {"HBRBC_SM_GREC": "0"}}
+            "grec_on": {"HBRBC_SM_GREC": "1"}, "grec_off": {"HBRBC_SM_GREC": "0"},
+            # every round through the kernels with the Value / Fake handlers
+            # (default: rounds >= 2 of a batch without injection run without them)
+            "lean_off": {"HBRBC_SM_LEAN": "0"}}
 
 
 def test_single_root_scenarios_on_host():
@@ -323,6 +326,48 @@ def test_single_root_state_machine_matches_host(n, form, monkeypatch):
                 assert got == ho[node], (form, world, i, node, got, ho[node])
                 assert faults[(i, node)] == hf[node], (form, world, i, node, faults[(i, node)],
                                                        hf[node])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,worlds", [(7, (1, 3)), (16, (1, 2)), (64, (1, 8))])
+def test_lean_rounds_multi_root_match_host(n, worlds):
+    """Batches without injected broadcasts (flags HBRBC_SM_NO_FAKE) run rounds
+    >= 2 through the lean kernels (sim.hip Sm::deliver<LEAN>); with several
+    roots (equivocating proposers, Sm<false>) every node's output, fault log
+    and the round count still equal the host restatement."""
+    from hbbft_amd.rbc_sim import SM_NO_FAKE, StateMachineRank, simulate
+    rng = random.Random(2000 + n)
+    insts = [i for i in make_instances(n, rng) + make_instances(n, rng, seed_tag=1)
+             if i.fake_from is None]
+    scn = Scenario(n, insts)
+    assert scn.roots > 1
+    assert StateMachineRank.from_scenario(scn, 0, 1).flags == SM_NO_FAKE
+    ref = [host_run(inst) for inst in insts]
+    for world in worlds:
+        outs, faults, rounds = simulate(scn, world=world)
+        assert rounds == max(r[2] for r in ref), (world, rounds)
+        for i, (ho, hf, _) in enumerate(ref):
+            for node in range(n):
+                got = [] if outs[(i, node)] is None else [outs[(i, node)]]
+                assert got == ho[node], (world, i, node, got, ho[node])
+                assert faults[(i, node)] == hf[node], (world, i, node)
+
+
+@pytest.mark.gpu
+def test_lean_round_rejects_injected_records():
+    """A batch WITH a fake_from node marked HBRBC_SM_NO_FAKE anyway: its Fake
+    record reaches a lean round, which reports it (emitted[1] bit 1) and the
+    driver raises instead of dropping the message."""
+    from hbbft_amd.rbc_sim import SM_NO_FAKE, StateMachineRank, data_plane, run_rounds
+    n = 7
+    insts = [i for i in make_instances(n, random.Random(3)) if i.fake_from is not None]
+    scn = Scenario(n, insts)
+    ok, dec, _, _ = data_plane(scn, 0)
+    sm = StateMachineRank.from_scenario(scn, 0, 1, 0, 24, 64, ok, dec)
+    assert sm.flags == 0
+    sm.flags = SM_NO_FAKE
+    with pytest.raises(RuntimeError, match="Value or Fake record"):
+        run_rounds([sm])
 
 
 @pytest.mark.gpu
