@@ -39,6 +39,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 // Compile-time A/B switches of the one-root round kernel (round 4):
 // HB_SM_CACHE keeps the inbox loop's 32-sender mask word in registers,
@@ -71,20 +72,12 @@
 #ifndef HB_SM_CONSTAS
 #define HB_SM_CONSTAS 1
 #endif
-#ifndef HB_SM_PREFETCH
-#define HB_SM_PREFETCH 1
-#endif
 
 namespace hbrbc {
 
 namespace {
 
 constexpr uint32_t kNone = 0xFFu;
-// the inbox as global-address-space words (the prefetch's vector loads)
-typedef __attribute__((address_space(1))) const uint32_t gu32;
-__device__ __forceinline__ uint32_t rfl_u(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
 
 // message kinds (broadcast::Message, message.rs:13-24) + the fake block
 enum { K_VALUE = 0, K_ECHO = 1, K_READY = 2, K_CAN_DECODE = 3, K_ECHO_HASH = 4, K_FAKE = 5 };
@@ -582,11 +575,16 @@ struct Sm {
     // record of those kinds sets `bad` (the launch reports it, emitted[1] bit 1).
     bool bad = false;
     template <bool LEAN>
-    __device__ __forceinline__ void deliver(int s, uint32_t h0) {
+    // k0: the kind of the step's first record, which a merged Echo /
+    // EchoHash step shares with its second (the class): wave-uniform in the
+    // global-records kernel, so the dispatch is a scalar branch even where the
+    // lanes of a merged step take different kinds (the per-lane kind is only
+    // the handler's `full` operand)
+    __device__ __forceinline__ void deliver(int s, uint32_t h0, uint32_t k0) {
         const uint32_t kind = h0 & 0xFFu, c0 = (h0 >> 8) & 0xFFu;
         const uint32_t j = (h0 >> 16) & 0xFFu, t = (h0 >> 24) & 0xFFu;
         if constexpr (LEAN) {
-            switch (kind) {
+            switch (k0) {
                 case K_ECHO:
                 case K_ECHO_HASH: handle_echo_any(s, c0, j, t, kind == K_ECHO); break;
                 case K_READY: handle_ready_core(s, c0, true); break;
@@ -597,7 +595,7 @@ struct Sm {
             }
             return;
         }
-        switch (kind) {
+        switch (k0) {
             case K_VALUE: {
                 // the proposer's Value to us: proof (value_root[me], me, value_tamper[me]);
                 // an explicit root (fake Values) carries proof (c0, me, 0)
@@ -655,46 +653,43 @@ struct SmLayout {
 // The inbox of one instance, walked sender by sender in order: sender s's
 // record count and records sit at index idx(s) = ((s / R) * count + inst) * R
 // + s % R of the all-gathered inbox (sm_in_block), or at s in a staged LDS
-// copy (R = 0: no blocks).  The index moves incrementally -- +1, and (count
-// - 1) * R more after the last sender of a rank's block -- instead of the
+// copy (R = 0: no blocks).  The count and record pointers move incrementally
+// -- one sender, and (count - 1) * R more after the last sender of a rank's
+// block -- instead of the
 // per-sender 32-bit division and 64-bit products of sm_in_block, which the
 // ISA showed as ~50 scalar instructions per sender ahead of every record
 // read (round 5: the inbox loop was bound by the CU's scalar unit,
 // profiles/r5e_sm_counters.txt).  P: the pointer type (the global-records
 // kernel keeps the constant address space).
-template <class P, class Q>
+template <class P>
 struct SmInbox {
-    P cnt, rec;        // counts [idx], records [idx][MR]
-    Q vcnt, vrec;      // the same through the prefetch's pointer type
-    size_t idx, jump;  // jump: (count - 1) * R
+    P cp, rp;          // this sender's count word and first record
+    size_t jump, jumpr;  // (count - 1) * R count words, and their records
     uint32_t rr, R, MR, max_out;
-    __device__ __forceinline__ uint32_t clamp(uint32_t c) const {
-        c &= 0x7FFFFFFFu;
+    __device__ __forceinline__ uint32_t count() const {
+        const uint32_t c = *cp & 0x7FFFFFFFu;
         return c < max_out ? c : max_out;
     }
-    __device__ __forceinline__ uint32_t count() const { return clamp(cnt[idx]); }
-    __device__ __forceinline__ P recs() const { return rec + idx * MR; }
-    __device__ __forceinline__ uint32_t vcount_raw() const { return vcnt[idx]; }
-    __device__ __forceinline__ Q vrecs() const { return vrec + idx * MR; }
+    __device__ __forceinline__ P recs() const { return rp; }
     __device__ __forceinline__ void advance() {
-        ++idx;
+        ++cp;
+        rp += MR;
         if (R && ++rr == R) {
             rr = 0;
-            idx += jump;
+            cp += jump;
+            rp += jumpr;
         }
     }
 };
-template <class P, class Q>
-__device__ __forceinline__ SmInbox<P, Q> sm_inbox(P cnt, P rec, Q vcnt, Q vrec, size_t inst,
-                                                  size_t count, uint32_t R, uint32_t MR,
-                                                  uint32_t max_out) {
-    SmInbox<P, Q> b;
-    b.cnt = cnt;
-    b.rec = rec;
-    b.vcnt = vcnt;
-    b.vrec = vrec;
-    b.idx = R ? inst * R : 0;   // sender 0: block 0, row 0
+template <class P>
+__device__ __forceinline__ SmInbox<P> sm_inbox(P cnt, P rec, size_t inst, size_t count, uint32_t R,
+                                               uint32_t MR, uint32_t max_out) {
+    SmInbox<P> b;
+    const size_t idx = R ? inst * R : 0;   // sender 0: block 0, row 0
+    b.cp = cnt + idx;
+    b.rp = rec + idx * MR;
     b.jump = R ? (count - 1) * R : 0;
+    b.jumpr = b.jump * MR;
     b.rr = 0;
     b.R = R;
     b.MR = MR;
@@ -755,92 +750,54 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     } else {
         m.drop = m.role == R_SILENT;
         const bool faker = !LEAN && a.fake_from[inst] == (uint8_t)me;
-        // this node's word of a record's recipient mask (the record pointer
+        // this node's bit in a record's recipient mask (the record pointer
         // keeps its address space: see HB_SM_CONSTAS)
         const int mw = me >> 5;
-        const uint32_t rw = 1 + W, mb = (uint32_t)(me & 31);
-        // HB_SM_PREFETCH: sender s + 1's count and the headers and mask words
-        // of its first two records are in flight while sender s is handled
-        // (vector loads: their waits do not drain the LDS counter the
-        // handlers' state accesses wait on)
-        const bool two = a.max_out >= 2;
-        uint32_t pc = 0, ph0 = 0, ph1 = 0, pm0 = 0, pm1 = 0;
-        auto fetch = [&]() {
-            const auto q = in.vrecs();
-            const auto q1 = q + (two ? rw : 0u);
-            pc = in.vcount_raw();
-            ph0 = q[0];
-            pm0 = q[1 + mw];
-            ph1 = q1[0];
-            pm1 = q1[1 + mw];
-        };
-        if (HB_SM_PREFETCH) fetch();
+        auto rbit = [&](auto r) -> bool { return (r[1 + mw] >> (me & 31)) & 1u; };
         // (no lane test for s == me: no record targets its own sender, so
         // that lane's bit is clear -- a divergent `continue` cost exec-mask
         // work on every sender)
+        // Echo / EchoHash kinds as a bit set (the merge test below)
+        constexpr uint32_t kEchoKinds = (1u << K_ECHO) | (1u << K_ECHO_HASH);
+        // the global-records kernel's records are wave-uniform (scalar loads)
+        constexpr bool UNI = !std::is_same<decltype(in.recs()), const uint32_t *>::value;
+        const uint32_t rw = 1 + W;
         for (int s = 0; s < n; ++s) {
             if (HB_SM_CACHE) m.em_focus(s >> 5);
-            const auto rs = in.recs();
-            uint32_t cnt, h0p = 0, h1p = 0, m0p = 0, m1p = 0;
-            if (HB_SM_PREFETCH) {
-                cnt = in.clamp(rfl_u(pc));
-                h0p = rfl_u(ph0);
-                h1p = rfl_u(ph1);
-                m0p = pm0;
-                m1p = pm1;
-                if (s + 1 < n) {
-                    in.advance();
-                    fetch();
-                }
-            } else {
-                cnt = in.count();
-                in.advance();
-            }
-            // header and this node's mask word of record e
-            auto get = [&](uint32_t e, uint32_t &h, uint32_t &mk) {
-                if (HB_SM_PREFETCH && e < 2) {
-                    h = e ? h1p : h0p;
-                    mk = e ? m1p : m0p;
-                } else {
-                    const auto r = rs + (size_t)e * rw;
-                    h = r[0];
-                    mk = r[1 + mw];
-                }
-            };
-            for (uint32_t e = 0; e < cnt; ++e) {
-                uint32_t h0, mk0;
-                get(e, h0, mk0);
+            const uint32_t cnt = in.count();
+            auto r = in.recs();
+            in.advance();
+            for (uint32_t e = 0; e < cnt; ++e, r += rw) {
+                uint32_t h0 = r[0];
                 const uint32_t k0 = h0 & 0xFFu;
-                bool hit = (mk0 >> mb) & 1u;
+                bool hit = rbit(r);
                 // An Echo and an EchoHash of the same sender in a row whose
                 // targets do not overlap at this node (handle_value emits
                 // Echo to all but the right nodes, EchoHash to the right
                 // ones): this node handles at most one of them, so both are
-                // taken in one step through the merged handler.
-                // The step is taken only when every lane of the wave can take
-                // it (a sequential step is always exact), so the record index
-                // stays wave-uniform and the global-records kernel reads the
-                // records with scalar loads.
-                if (HB_SM_MERGE) {
-                    bool pair = false, hit2 = false;
-                    uint32_t h1 = 0;
-                    if ((k0 == K_ECHO || k0 == K_ECHO_HASH) && e + 1 < cnt) {
-                        uint32_t mk1;
-                        get(e + 1, h1, mk1);
-                        const uint32_t k1 = h1 & 0xFFu;
-                        hit2 = (mk1 >> mb) & 1u;
-                        pair = (k1 == K_ECHO || k1 == K_ECHO_HASH) && k1 != k0 && !(hit && hit2);
-                    }
-                    if (__all(pair)) {
-                        ++e;
-                        if (hit2) {
-                            h0 = h1;
-                            hit = true;
+                // taken in one step through the merged handler (a sequential
+                // step is always exact).  In the global-records kernel the
+                // step is taken only when every lane of the wave can take it,
+                // so the record index stays wave-uniform (scalar loads, and
+                // the kind tests are scalar branches).
+                if (HB_SM_MERGE && ((kEchoKinds >> k0) & 1u) && e + 1 < cnt) {
+                    const uint32_t h1 = r[rw];
+                    const uint32_t k1 = h1 & 0xFFu;
+                    if (((kEchoKinds >> k1) & 1u) && k1 != k0) {
+                        const bool hit2 = rbit(r + rw);
+                        const bool ok = !(hit && hit2);
+                        if (UNI ? __all(ok) : ok) {
+                            ++e;
+                            r += rw;
+                            if (hit2) {
+                                h0 = h1;
+                                hit = true;
+                            }
                         }
                     }
                 }
                 if (!hit) continue;
-                m.template deliver<LEAN>(s, h0);
+                m.template deliver<LEAN>(s, h0, k0);
                 if (faker && !(m.FLAGS() & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
                     m.FLAGS() |= FL_FAKE_DONE;
@@ -879,8 +836,8 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     uint8_t *st = a.state + inst * a.nodes * sm_state_bytes(n, a.roots);
     sm_node<ONE, LEAN>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
             a.decode_ok + inst * a.roots,
-            sm_inbox(a.in_count, a.in, (gu32 *)a.in_count, (gu32 *)a.in, inst, a.count,
-                     a.rows_per_rank, (uint32_t)MR, a.max_out));
+            sm_inbox<const uint32_t *>(a.in_count, a.in, inst, a.count, a.rows_per_rank,
+                                       (uint32_t)MR, a.max_out));
 }
 
 // Round kernel, staged form: a workgroup owns `ipb` whole instances (ipb x
@@ -958,14 +915,14 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
             sm_node<ONE, LEAN>(a, n, f, k, inst * nodes + local, inst, local,
                     lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
                     lds + o_dok + (size_t)li * C,
-                    sm_inbox(gcnt, gin, (gu32 *)a.in_count, (gu32 *)a.in, ui, a.count,
-                             a.rows_per_rank, (uint32_t)MR, a.max_out));
+                    sm_inbox<cu32 *>(gcnt, gin, ui, a.count, a.rows_per_rank, (uint32_t)MR,
+                                     a.max_out));
         } else {
             const uint32_t *cb = lcnt + (size_t)li * n;
             const uint32_t *rb = lrec + (size_t)li * n * MR;
             sm_node<ONE, LEAN>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
                     lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
-                    sm_inbox(cb, rb, cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
+                    sm_inbox<const uint32_t *>(cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
         }
     }
     __syncthreads();

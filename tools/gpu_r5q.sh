@@ -20,6 +20,8 @@ for rep in 1 2 3; do
     sed "s/^{/{\"lean\": $2, /" $OUT/b.json >> $OUT/sm_bench.jsonl
   done
 done
+cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace -d $ROOT/$OUT/trace -o run -- python3 $ROOT/tools/sm_bench.py --reps 2 > $ROOT/$OUT/trace.log 2>&1
+rc=$?; cd $ROOT; echo "trace exit $rc"; if fatal $rc; then exit $rc; fi
 python3 -c "
 import json
 for l in open('$OUT/sm_bench.jsonl'):
