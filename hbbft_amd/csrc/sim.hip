@@ -309,7 +309,11 @@ struct Sm {
         return (len >= 32 ? 0xFFFFFFFFu : ((1u << len) - 1u)) << (lo - 32 * w);
     }
     __device__ __forceinline__ uint32_t all_but_me(int w) const {
-        return lin(w, 0, n) & ~((me >> 5) == w ? 1u << (me & 31) : 0u);
+        // lin(w, 0, n): whole words, then the partial last one (a few scalar
+        // ops instead of lin's clamps; it runs once per word of every send)
+        const int fw = n >> 5;
+        const uint32_t all = w < fw ? 0xFFFFFFFFu : (w == fw ? (1u << (n & 31)) - 1u : 0u);
+        return all & ~((me >> 5) == w ? 1u << (me & 31) : 0u);
     }
     // right_nodes(me) (broadcast.rs:476-485): [me - f, me) on the circle
     __device__ __forceinline__ uint32_t right_mask(int w) const {
@@ -319,19 +323,6 @@ struct Sm {
     template <class M>
     __device__ __forceinline__ void targets_w(uint32_t *r, M mask) {
         for (int w = 0; w < W; ++w) r[1 + w] = mask(w);
-    }
-
-    // the recipient mask of record r: bit i set iff pred(i), each word built
-    // in a register and stored once (the caller fills every emitted record)
-    template <class P>
-    __device__ __forceinline__ void targets(uint32_t *r, P pred) {
-        for (int w = 0; w < W; ++w) {
-            uint32_t mk = 0;
-            const int hi = n - 32 * w < 32 ? n - 32 * w : 32;
-            for (int b = 0; b < hi; ++b)
-                if (pred(32 * w + b)) mk |= 1u << b;
-            r[1 + w] = mk;
-        }
     }
 
     // emission as the node's own step (subject to its role)
@@ -568,13 +559,15 @@ struct Sm {
         }
     }
 
-    // h0: the record's header word.  LEAN: the rounds >= 2 of a batch without
-    // injected broadcasts, whose inboxes hold only Echo / EchoHash / Ready /
-    // CanDecode records (Values go out in round 0 only, Fake records only from
-    // a fake_from node): the Value and Fake handlers are not compiled in, and a
-    // record of those kinds sets `bad` (the launch reports it, emitted[1] bit 1).
+    // h0: the record's header word.  LV (handler set): 0 every handler; in a
+    // batch without injected broadcasts (no Fake records: those come only
+    // from a fake_from node) 1 -- round 1: no Fake handler -- and 2 -- rounds
+    // >= 2, whose inboxes hold only Echo / EchoHash / Ready / CanDecode
+    // records (Values go out in round 0 only): no Value handler either.  A
+    // record of a kind not compiled in sets `bad` (the launch reports it,
+    // emitted[1] bit 1).
     bool bad = false;
-    template <bool LEAN>
+    template <int LV>
     // k0: the kind of the step's first record, which a merged Echo /
     // EchoHash step shares with its second (the class): wave-uniform in the
     // global-records kernel, so the dispatch is a scalar branch even where the
@@ -583,16 +576,16 @@ struct Sm {
     __device__ __forceinline__ void deliver(int s, uint32_t h0, uint32_t k0) {
         const uint32_t kind = h0 & 0xFFu, c0 = (h0 >> 8) & 0xFFu;
         const uint32_t j = (h0 >> 16) & 0xFFu, t = (h0 >> 24) & 0xFFu;
-        if constexpr (LEAN) {
-            switch (k0) {
-                case K_ECHO:
-                case K_ECHO_HASH: handle_echo_any(s, c0, j, t, kind == K_ECHO); break;
-                case K_READY: handle_ready_core(s, c0, true); break;
-                case K_CAN_DECODE: handle_can_decode(s, c0); break;
-                case K_VALUE:
-                case K_FAKE: bad = true; break;
-                default: break;
-            }
+        if constexpr (LV == 2) {
+            // the round's common kinds first (a switch became a compare tree)
+            if (((1u << K_ECHO) | (1u << K_ECHO_HASH)) >> k0 & 1u)
+                handle_echo_any(s, c0, j, t, kind == K_ECHO);
+            else if (k0 == K_READY)
+                handle_ready_core(s, c0, true);
+            else if (k0 == K_CAN_DECODE)
+                handle_can_decode(s, c0);
+            else if (k0 == K_VALUE || k0 == K_FAKE)
+                bad = true;
             return;
         }
         switch (k0) {
@@ -613,7 +606,10 @@ struct Sm {
                 break;
             case K_READY: handle_ready_core(s, c0, true); break;
             case K_CAN_DECODE: handle_can_decode(s, c0); break;
-            case K_FAKE: handle_fake(s, c0); break;
+            case K_FAKE:
+                if constexpr (LV == 0) handle_fake(s, c0);
+                else bad = true;
+                break;
             default: break;
         }
     }
@@ -621,6 +617,27 @@ struct Sm {
 
 template <bool ONE>
 __device__ __forceinline__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bool may_send) {   // 378-410
+    if constexpr (ONE) {
+        // one root: the entry is bit s of the Ready mask (stored root 0), and
+        // the common path -- a fresh Ready: set the bit, count it -- is
+        // predicated; the fault, the sends and the output stay behind
+        // branches, each condition read after the step before it ran (as in
+        // the branchy form below: send_ready moves the count)
+        const int w = s >> 5;
+        const uint32_t b = 1u << (s & 31);
+        uint4 m4 = em_get(w);
+        const bool had = m4.w & b;
+        if (__builtin_expect(had && c != 0u, 0)) fault(s, F_MULTIPLE_READYS);
+        const bool go = !had;
+        m4.w |= go ? b : 0u;
+        em_put(w, m4);
+        r_cr += go ? 1 : 0;
+        if (__builtin_expect(go && may_send && r_cr == f + 1 && !(r_flags & FL_READY_SENT), 0))
+            send_ready(c);
+        if (__builtin_expect(go && r_cr == 2 * f + 1, 0)) send_echo_remaining(c);
+        if (go) compute_output(c);
+        return;
+    }
     const uint32_t old = READY(s);
     if (old) {
         if (old - 1 != c) fault(s, F_MULTIPLE_READYS);
@@ -700,7 +717,7 @@ __device__ __forceinline__ SmInbox<P> sm_inbox(P cnt, P rec, size_t inst, size_t
 // Handles one node's inbox of the round (or, in round 0, the proposer's
 // broadcast()).  `st` is the instance's state block (stride sd = nodes),
 // `in` the instance's inbox at sender 0.
-template <bool ONE, bool LEAN, class Inbox>
+template <bool ONE, int LV, class Inbox>
 __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, int k, size_t g, size_t inst,
                         int local, uint8_t *st, const uint8_t *pok, const uint8_t *dok,
                         Inbox in) {
@@ -734,7 +751,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     m.faults = a.faults + g * (size_t)a.max_faults;
     m.nfault = a.fault_count[g];
     m.cache_in();
-    if (!LEAN && a.round == 0) {
+    if (LV == 0 && a.round == 0) {
         // the proposer's broadcast() (broadcast.rs:123-137, 170-225): its input
         // step goes out unfiltered (VirtualNet::send_input; only deliveries to
         // faulty nodes pass the adversary)
@@ -742,14 +759,32 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         if (me == m.proposer && !(m.FLAGS() & FL_VALUE_SENT)) {
             m.FLAGS() |= FL_VALUE_SENT;
             uint32_t *r = m.emit_rec(K_VALUE, kNone, 0, 0);
-            if (r)
-                m.targets(r, [&](int i) { return i != me && a.value_root[inst * n + i] != kNone; });
+            if (r) {
+                // every node but me with a Value: 32 independent byte loads
+                // per word (index clamped into the row), one wait, instead of
+                // a load and a branch per node
+                const uint8_t *vr = a.value_root + inst * n;
+                for (int w = 0; w < W; ++w) {
+                    uint32_t mk = 0;
+#pragma unroll
+                    for (int b = 0; b < 32; ++b) {
+                        const int i = 32 * w + b;
+                        const uint32_t v = vr[i < n ? i : n - 1];
+                        mk |= (uint32_t)(i < n && i != me && v != kNone) << b;
+                    }
+                    r[1 + w] = mk;
+                }
+            }
             const uint32_t c = a.value_root[inst * n + me];
             if (c != kNone) m.handle_value(me, c, (uint32_t)me, a.value_tamper[inst * n + me]);
         }
     } else {
         m.drop = m.role == R_SILENT;
-        const bool faker = !LEAN && a.fake_from[inst] == (uint8_t)me;
+        const bool is_faker = a.fake_from[inst] == (uint8_t)me;
+        const bool faker = LV == 0 && is_faker;
+        // (a smaller handler set has no injection: a fake_from node means the
+        // caller's HBRBC_SM_NO_FAKE was wrong, reported like a stray record)
+        if (LV > 0 && is_faker) m.bad = true;
         // this node's bit in a record's recipient mask (the record pointer
         // keeps its address space: see HB_SM_CONSTAS)
         const int mw = me >> 5;
@@ -797,7 +832,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
                     }
                 }
                 if (!hit) continue;
-                m.template deliver<LEAN>(s, h0, k0);
+                m.template deliver<LV>(s, h0, k0);
                 if (faker && !(m.FLAGS() & FL_FAKE_DONE)) {
                     // after the first delivered message (tests/broadcast.rs:73-97)
                     m.FLAGS() |= FL_FAKE_DONE;
@@ -813,7 +848,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
     a.fault_count[g] = m.nfault;
     if (m.nout) atomicAdd(a.emitted, m.nout);
     if (m.overflow) atomicOr(a.emitted + 1, 1u);
-    if (LEAN && m.bad) atomicOr(a.emitted + 1, 2u);
+    if (LV > 0 && m.bad) atomicOr(a.emitted + 1, 2u);
 }
 
 __device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t inst, int s) {
@@ -824,7 +859,7 @@ __device__ __forceinline__ size_t sm_in_block(const hbrbc_sm_args &a, size_t ins
 // Round kernel, global form: one thread per (instance, hosted node), state,
 // records and outcomes read where they lie.  For blocks whose staged copy
 // does not fit the LDS budget (sm_plan).
-template <bool ONE, bool LEAN>
+template <bool ONE, int LV>
 __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, int f, int k) {
     if (a.active && *a.active == 0u) return;   // quiescent: nothing was sent last round
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -834,7 +869,7 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
     if ((int)a.node_lo + local >= n) return;
     const size_t MR = (size_t)a.max_out * ((n + 31) / 32 + 1);
     uint8_t *st = a.state + inst * a.nodes * sm_state_bytes(n, a.roots);
-    sm_node<ONE, LEAN>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
+    sm_node<ONE, LV>(a, n, f, k, g, inst, local, st, a.proof_ok + inst * a.roots * 2 * n,
             a.decode_ok + inst * a.roots,
             sm_inbox<const uint32_t *>(a.in_count, a.in, inst, a.count, a.rows_per_rank,
                                        (uint32_t)MR, a.max_out));
@@ -855,7 +890,7 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
 // KB per instance), so the grid's blocks fit the chip in one round instead of
 // 1.3 (a second, mostly idle round of blocks), and the per-thread staging
 // loop over the records (a chain of dependent global loads) goes away.
-template <bool ONE, bool GREC, bool LEAN>
+template <bool ONE, bool GREC, int LV>
 __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, int f, int k,
                                                 int ipb) {
     extern __shared__ uint4 sm_lds4[];
@@ -912,7 +947,7 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
 #endif
             cu32 *gin = (cu32 *)a.in;
             cu32 *gcnt = (cu32 *)a.in_count;
-            sm_node<ONE, LEAN>(a, n, f, k, inst * nodes + local, inst, local,
+            sm_node<ONE, LV>(a, n, f, k, inst * nodes + local, inst, local,
                     lds + (size_t)li * nodes * sb, lds + o_pok + (size_t)li * C * 2 * n,
                     lds + o_dok + (size_t)li * C,
                     sm_inbox<cu32 *>(gcnt, gin, ui, a.count, a.rows_per_rank, (uint32_t)MR,
@@ -920,7 +955,7 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
         } else {
             const uint32_t *cb = lcnt + (size_t)li * n;
             const uint32_t *rb = lrec + (size_t)li * n * MR;
-            sm_node<ONE, LEAN>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
+            sm_node<ONE, LV>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
                     lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
                     sm_inbox<const uint32_t *>(cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
         }
@@ -930,10 +965,10 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
         reinterpret_cast<uint2 *>(gst)[i] = reinterpret_cast<const uint2 *>(lds)[i];
 }
 
-template <bool ONE, bool LEAN>
+template <bool ONE, int LV>
 __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
                                                               int k, int ipb) {
-    sm_round_staged<ONE, false, LEAN>(a, n, f, k, ipb);
+    sm_round_staged<ONE, false, LV>(a, n, f, k, ipb);
 }
 // The same at 4 waves/SIMD (128 VGPRs, a few spills instead of 162 VGPRs):
 // for launches whose LDS image leaves room for more than 3 waves per SIMD
@@ -942,20 +977,20 @@ __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, i
 #ifndef HB_SM_W4_WAVES
 #define HB_SM_W4_WAVES 4   // waves/SIMD of the "w4" forms (A/B: -DHB_SM_W4_WAVES=5)
 #endif
-template <bool ONE, bool LEAN>
+template <bool ONE, int LV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_staged_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
-    sm_round_staged<ONE, false, LEAN>(a, n, f, k, ipb);
+    sm_round_staged<ONE, false, LV>(a, n, f, k, ipb);
 }
-template <bool ONE, bool LEAN>
+template <bool ONE, int LV>
 __global__ __launch_bounds__(256) void sm_round_grec_kernel(hbrbc_sm_args a, int n, int f, int k,
                                                             int ipb) {
-    sm_round_staged<ONE, true, LEAN>(a, n, f, k, ipb);
+    sm_round_staged<ONE, true, LV>(a, n, f, k, ipb);
 }
-template <bool ONE, bool LEAN>
+template <bool ONE, int LV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_grec_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
-    sm_round_staged<ONE, true, LEAN>(a, n, f, k, ipb);
+    sm_round_staged<ONE, true, LV>(a, n, f, k, ipb);
 }
 
 }  // namespace
@@ -971,8 +1006,8 @@ static size_t sm_lds_bytes(const hbrbc_sm_args &a, int n, int ipb, bool grec = f
     return ((size_t)ipb * per + 15) & ~(size_t)15;
 }
 
-// One instantiation set per handler set (LEAN: see Sm::deliver).
-template <bool LEAN>
+// One instantiation set per handler set (LV: see Sm::deliver).
+template <int LV>
 static hipError_t launch_sm_form(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s) {
     const size_t threads = a.count * a.nodes;
     const char *e = getenv("HBRBC_SM_STAGED");   // 0: the global form (A/B)
@@ -995,32 +1030,34 @@ static hipError_t launch_sm_form(const hbrbc_sm_args &a, int n, int f, int k, hi
         const char *w4e = getenv("HBRBC_SM_W4");
         const bool w4 = w4e ? !strcmp(w4e, "1")
                             : (163840 / lds) * ((threads_pb + 63) / 64) > 12;
-        auto kern = grec ? (a.roots == 1 ? (w4 ? sm_round_grec_w4_kernel<true, LEAN>
-                                               : sm_round_grec_kernel<true, LEAN>)
-                                         : (w4 ? sm_round_grec_w4_kernel<false, LEAN>
-                                               : sm_round_grec_kernel<false, LEAN>))
-                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true, LEAN>
-                                               : sm_round_staged_kernel<true, LEAN>)
-                                         : (w4 ? sm_round_staged_w4_kernel<false, LEAN>
-                                               : sm_round_staged_kernel<false, LEAN>));
+        auto kern = grec ? (a.roots == 1 ? (w4 ? sm_round_grec_w4_kernel<true, LV>
+                                               : sm_round_grec_kernel<true, LV>)
+                                         : (w4 ? sm_round_grec_w4_kernel<false, LV>
+                                               : sm_round_grec_kernel<false, LV>))
+                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true, LV>
+                                               : sm_round_staged_kernel<true, LV>)
+                                         : (w4 ? sm_round_staged_w4_kernel<false, LV>
+                                               : sm_round_staged_kernel<false, LV>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3((unsigned)threads_pb), lds, s, a, n, f, k, ipb);
         return hipGetLastError();
     }
     const unsigned blocks = (unsigned)((threads + 255) / 256);
     if (a.roots == 1)
-        hipLaunchKernelGGL((sm_round_kernel<true, LEAN>), dim3(blocks), dim3(256), 0, s, a, n, f, k);
+        hipLaunchKernelGGL((sm_round_kernel<true, LV>), dim3(blocks), dim3(256), 0, s, a, n, f, k);
     else
-        hipLaunchKernelGGL((sm_round_kernel<false, LEAN>), dim3(blocks), dim3(256), 0, s, a, n, f, k);
+        hipLaunchKernelGGL((sm_round_kernel<false, LV>), dim3(blocks), dim3(256), 0, s, a, n, f, k);
     return hipGetLastError();
 }
 
 hipError_t launch_sm_round(const hbrbc_sm_args &a, int n, int f, int k, hipStream_t s) {
     if (a.count * a.nodes == 0) return hipSuccess;
-    // the lean handler set for rounds >= 2 of a batch the caller marks as
+    // the smaller handler sets for rounds >= 1 of a batch the caller marks as
     // having no injected broadcasts (HBRBC_SM_LEAN=0: never, A/B)
     const char *le = getenv("HBRBC_SM_LEAN");
-    const bool lean = (a.flags & HBRBC_SM_NO_FAKE) && a.round >= 2 && !(le && !strcmp(le, "0"));
-    return lean ? launch_sm_form<true>(a, n, f, k, s) : launch_sm_form<false>(a, n, f, k, s);
+    const int lv = (a.flags & HBRBC_SM_NO_FAKE) && !(le && !strcmp(le, "0"))
+                       ? (a.round >= 2 ? 2 : (a.round == 1 ? 1 : 0)) : 0;
+    return lv == 2 ? launch_sm_form<2>(a, n, f, k, s)
+                   : (lv == 1 ? launch_sm_form<1>(a, n, f, k, s) : launch_sm_form<0>(a, n, f, k, s));
 }
 
 }  // namespace hbrbc

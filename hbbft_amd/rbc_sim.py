@@ -353,8 +353,8 @@ def _check_batch(ranks, h, r0, own=None):
     for i in range(h.shape[1]):
         fl = int(h[:, i, 1].max())
         if fl & 2:
-            raise RuntimeError("state machine: a Value or Fake record reached a round run "
-                               "without those handlers (hbrbc_sm_args.flags)")
+            raise RuntimeError("state machine: a Value / Fake record or a fake_from node reached "
+                               "a round run without those handlers (hbrbc_sm_args.flags)")
         if fl:
             raise RuntimeError("state machine: a node emitted more than %d messages in a round"
                                % ranks[0].max_out)

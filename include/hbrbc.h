@@ -524,11 +524,12 @@ typedef struct hbrbc_sm_args {
                                      (every sender's previous round emitted nothing: the
                                      network is quiescent), so a host can enqueue several
                                      rounds and read the emitted counts back once */
-    uint32_t flags;               /* HBRBC_SM_NO_FAKE: no instance has a fake_from node, so the
-                                     inboxes of rounds >= 2 hold only Echo, EchoHash, Ready and
-                                     CanDecode records and those rounds run a kernel without the
-                                     Value / Fake handlers (a record of another kind there sets
-                                     emitted[1] bit 1, the caller's error) */
+    uint32_t flags;               /* HBRBC_SM_NO_FAKE: no instance has a fake_from node, so no
+                                     inbox holds a Fake record and those of rounds >= 2 hold only
+                                     Echo, EchoHash, Ready and CanDecode records: round 1 runs a
+                                     kernel without the Fake handler, rounds >= 2 one without the
+                                     Value handler too (a record of a kind left out, or a
+                                     fake_from node, sets emitted[1] bit 1, the caller's error) */
 } hbrbc_sm_args;
 #define HBRBC_SM_NO_FAKE 1u
 size_t hbrbc_sm_state_bytes(size_t n, size_t roots);

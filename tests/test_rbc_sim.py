@@ -356,8 +356,9 @@ def test_lean_rounds_multi_root_match_host(n, worlds):
 @pytest.mark.gpu
 def test_lean_round_rejects_injected_records():
     """A batch WITH a fake_from node marked HBRBC_SM_NO_FAKE anyway: its Fake
-    record reaches a lean round, which reports it (emitted[1] bit 1) and the
-    driver raises instead of dropping the message."""
+    node reaches a round run without the Fake handler, which reports it
+    (emitted[1] bit 1), and the driver raises instead of dropping the
+    injection."""
     from hbbft_amd.rbc_sim import SM_NO_FAKE, StateMachineRank, data_plane, run_rounds
     n = 7
     insts = [i for i in make_instances(n, random.Random(3)) if i.fake_from is not None]
@@ -366,7 +367,7 @@ def test_lean_round_rejects_injected_records():
     sm = StateMachineRank.from_scenario(scn, 0, 1, 0, 24, 64, ok, dec)
     assert sm.flags == 0
     sm.flags = SM_NO_FAKE
-    with pytest.raises(RuntimeError, match="Value or Fake record"):
+    with pytest.raises(RuntimeError, match="without those handlers"):
         run_rounds([sm])
 
 
