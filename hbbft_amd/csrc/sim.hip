@@ -155,6 +155,7 @@ struct Sm {
     uint4 cache = {0u, 0u, 0u, 0u};
     int cw = -1;
     __device__ __forceinline__ uint4 em_get(int w) const {
+#if HB_SM_CACHE
         // a select of values, not of addresses (a pointer select between the
         // register copy and LDS would put the whole Sm object on the stack)
         // -- LLVM folds "if (c) v = *p else v = *q" into a load through a
@@ -167,8 +168,14 @@ struct Sm {
             v = em[(size_t)w * sd];
         }
         return v;
+#else
+        // (no register copy: the compiler did not fold the never-taken
+        // register arm away, and its lane-mask select ran on every access)
+        return em[(size_t)w * sd];
+#endif
     }
     __device__ __forceinline__ void em_put(int w, const uint4 &v) {
+#if HB_SM_CACHE
         if (w == cw) {
             uint4 t = v;
             __asm__ volatile("" : "+v"(t.x), "+v"(t.y), "+v"(t.z), "+v"(t.w));
@@ -176,9 +183,12 @@ struct Sm {
         } else {
             em[(size_t)w * sd] = v;
         }
+#else
+        em[(size_t)w * sd] = v;
+#endif
     }
     __device__ __forceinline__ void em_focus(int w) {   // w uniform across the wave
-        if constexpr (ONE) {
+        if constexpr (ONE && HB_SM_CACHE) {
             if (w == cw) return;
             if (cw >= 0) em[(size_t)cw * sd] = cache;
             cache = em[(size_t)w * sd];
@@ -186,7 +196,7 @@ struct Sm {
         }
     }
     __device__ __forceinline__ void em_flush() {
-        if constexpr (ONE) {
+        if constexpr (ONE && HB_SM_CACHE) {
             if (cw >= 0) em[(size_t)cw * sd] = cache;
             cw = -1;
         }
@@ -788,6 +798,8 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         // this node's bit in a record's recipient mask (the record pointer
         // keeps its address space: see HB_SM_CONSTAS)
         const int mw = me >> 5;
+        // (a scalar load of both mask words of the wave's nodes, each lane
+        // picking its own, measured slower at N=128: 0.78 vs 0.765 ms)
         auto rbit = [&](auto r) -> bool { return (r[1 + mw] >> (me & 31)) & 1u; };
         // (no lane test for s == me: no record targets its own sender, so
         // that lane's bit is clear -- a divergent `continue` cost exec-mask
