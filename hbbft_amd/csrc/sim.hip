@@ -687,9 +687,12 @@ struct SmLayout {
 // ISA showed as ~50 scalar instructions per sender ahead of every record
 // read (round 5: the inbox loop was bound by the CU's scalar unit,
 // profiles/r5e_sm_counters.txt).  P: the pointer type (the global-records
-// kernel keeps the constant address space).
-template <class P>
+// kernel keeps the constant address space).  WI: every lane of a wave walks
+// the same instance's inbox (the LDS-staged kernel at nodes % 64 == 0), so a
+// count or header read per lane is moved to a scalar register.
+template <class P, bool WI = false>
 struct SmInbox {
+    static constexpr bool kWaveInst = WI;
     P cp, rp;          // this sender's count word and first record
     size_t jump, jumpr;  // (count - 1) * R count words, and their records
     uint32_t rr, R, MR, max_out;
@@ -708,10 +711,10 @@ struct SmInbox {
         }
     }
 };
-template <class P>
-__device__ __forceinline__ SmInbox<P> sm_inbox(P cnt, P rec, size_t inst, size_t count, uint32_t R,
-                                               uint32_t MR, uint32_t max_out) {
-    SmInbox<P> b;
+template <class P, bool WI = false>
+__device__ __forceinline__ SmInbox<P, WI> sm_inbox(P cnt, P rec, size_t inst, size_t count,
+                                                   uint32_t R, uint32_t MR, uint32_t max_out) {
+    SmInbox<P, WI> b;
     const size_t idx = R ? inst * R : 0;   // sender 0: block 0, row 0
     b.cp = cnt + idx;
     b.rp = rec + idx * MR;
@@ -806,16 +809,23 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         // work on every sender)
         // Echo / EchoHash kinds as a bit set (the merge test below)
         constexpr uint32_t kEchoKinds = (1u << K_ECHO) | (1u << K_ECHO_HASH);
-        // the global-records kernel's records are wave-uniform (scalar loads)
-        constexpr bool UNI = !std::is_same<decltype(in.recs()), const uint32_t *>::value;
+        // wave-uniform records: the global-records kernel's (scalar loads),
+        // and an LDS-staged inbox whose waves each hold one instance (values
+        // read per lane, equal in every lane, moved to scalar registers: the
+        // kind tests and the record loop become scalar branches)
+        constexpr bool UNI = Inbox::kWaveInst ||
+                             !std::is_same<decltype(in.recs()), const uint32_t *>::value;
+        auto uni = [](uint32_t v) {
+            return UNI ? (uint32_t)__builtin_amdgcn_readfirstlane((int)v) : v;
+        };
         const uint32_t rw = 1 + W;
         for (int s = 0; s < n; ++s) {
             if (HB_SM_CACHE) m.em_focus(s >> 5);
-            const uint32_t cnt = in.count();
+            const uint32_t cnt = uni(in.count());
             auto r = in.recs();
             in.advance();
             for (uint32_t e = 0; e < cnt; ++e, r += rw) {
-                uint32_t h0 = r[0];
+                uint32_t h0 = uni(r[0]);
                 const uint32_t k0 = h0 & 0xFFu;
                 bool hit = rbit(r);
                 // An Echo and an EchoHash of the same sender in a row whose
@@ -828,7 +838,7 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
                 // so the record index stays wave-uniform (scalar loads, and
                 // the kind tests are scalar branches).
                 if (HB_SM_MERGE && ((kEchoKinds >> k0) & 1u) && e + 1 < cnt) {
-                    const uint32_t h1 = r[rw];
+                    const uint32_t h1 = uni(r[rw]);
                     const uint32_t k1 = h1 & 0xFFu;
                     if (((kEchoKinds >> k1) & 1u) && k1 != k0) {
                         const bool hit2 = rbit(r + rw);
@@ -902,7 +912,7 @@ __global__ __launch_bounds__(256) void sm_round_kernel(hbrbc_sm_args a, int n, i
 // KB per instance), so the grid's blocks fit the chip in one round instead of
 // 1.3 (a second, mostly idle round of blocks), and the per-thread staging
 // loop over the records (a chain of dependent global loads) goes away.
-template <bool ONE, bool GREC, int LV>
+template <bool ONE, bool GREC, int LV, bool WI = false>
 __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, int f, int k,
                                                 int ipb) {
     extern __shared__ uint4 sm_lds4[];
@@ -969,7 +979,7 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
             const uint32_t *rb = lrec + (size_t)li * n * MR;
             sm_node<ONE, LV>(a, n, f, k, inst * nodes + local, inst, local, lds + (size_t)li * nodes * sb,
                     lds + o_pok + (size_t)li * C * 2 * n, lds + o_dok + (size_t)li * C,
-                    sm_inbox<const uint32_t *>(cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
+                    sm_inbox<const uint32_t *, WI>(cb, rb, 0, 1, 0, (uint32_t)MR, a.max_out));
         }
     }
     __syncthreads();
@@ -977,10 +987,11 @@ __device__ __forceinline__ void sm_round_staged(const hbrbc_sm_args &a, int n, i
         reinterpret_cast<uint2 *>(gst)[i] = reinterpret_cast<const uint2 *>(lds)[i];
 }
 
-template <bool ONE, int LV>
+// WI: nodes % 64 == 0, every wave one instance (SmInbox)
+template <bool ONE, int LV, bool WI>
 __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, int n, int f,
                                                               int k, int ipb) {
-    sm_round_staged<ONE, false, LV>(a, n, f, k, ipb);
+    sm_round_staged<ONE, false, LV, WI>(a, n, f, k, ipb);
 }
 // The same at 4 waves/SIMD (128 VGPRs, a few spills instead of 162 VGPRs):
 // for launches whose LDS image leaves room for more than 3 waves per SIMD
@@ -989,10 +1000,10 @@ __global__ __launch_bounds__(256) void sm_round_staged_kernel(hbrbc_sm_args a, i
 #ifndef HB_SM_W4_WAVES
 #define HB_SM_W4_WAVES 4   // waves/SIMD of the "w4" forms (A/B: -DHB_SM_W4_WAVES=5)
 #endif
-template <bool ONE, int LV>
+template <bool ONE, int LV, bool WI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HB_SM_W4_WAVES, HB_SM_W4_WAVES))) void
 sm_round_staged_w4_kernel(hbrbc_sm_args a, int n, int f, int k, int ipb) {
-    sm_round_staged<ONE, false, LV>(a, n, f, k, ipb);
+    sm_round_staged<ONE, false, LV, WI>(a, n, f, k, ipb);
 }
 template <bool ONE, int LV>
 __global__ __launch_bounds__(256) void sm_round_grec_kernel(hbrbc_sm_args a, int n, int f, int k,
@@ -1042,14 +1053,21 @@ static hipError_t launch_sm_form(const hbrbc_sm_args &a, int n, int f, int k, hi
         const char *w4e = getenv("HBRBC_SM_W4");
         const bool w4 = w4e ? !strcmp(w4e, "1")
                             : (163840 / lds) * ((threads_pb + 63) / 64) > 12;
+        // every wave one instance: scalar record dispatch (HBRBC_SM_WI=0: off, A/B)
+        const char *wie = getenv("HBRBC_SM_WI");
+        const bool wi = a.nodes % 64 == 0 && !(wie && !strcmp(wie, "0"));
         auto kern = grec ? (a.roots == 1 ? (w4 ? sm_round_grec_w4_kernel<true, LV>
                                                : sm_round_grec_kernel<true, LV>)
                                          : (w4 ? sm_round_grec_w4_kernel<false, LV>
                                                : sm_round_grec_kernel<false, LV>))
-                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true, LV>
-                                               : sm_round_staged_kernel<true, LV>)
-                                         : (w4 ? sm_round_staged_w4_kernel<false, LV>
-                                               : sm_round_staged_kernel<false, LV>));
+                         : wi ? (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true, LV, true>
+                                                    : sm_round_staged_kernel<true, LV, true>)
+                                              : (w4 ? sm_round_staged_w4_kernel<false, LV, true>
+                                                    : sm_round_staged_kernel<false, LV, true>))
+                         : (a.roots == 1 ? (w4 ? sm_round_staged_w4_kernel<true, LV, false>
+                                               : sm_round_staged_kernel<true, LV, false>)
+                                         : (w4 ? sm_round_staged_w4_kernel<false, LV, false>
+                                               : sm_round_staged_kernel<false, LV, false>));
         hipLaunchKernelGGL(kern, dim3(blocks), dim3((unsigned)threads_pb), lds, s, a, n, f, k, ipb);
         return hipGetLastError();
     }

@@ -285,7 +285,10 @@ SM_FORMS = {"staged_w4": {"HBRBC_SM_W4": "1"}, "staged_w3": {"HBRBC_SM_W4": "0"}
             "grec_on": {"HBRBC_SM_GREC": "1"}, "grec_off": {"HBRBC_SM_GREC": "0"},
             # every round through the kernels with the Value / Fake handlers
             # (default: rounds >= 2 of a batch without injection run without them)
-            "lean_off": {"HBRBC_SM_LEAN": "0"}}
+            "lean_off": {"HBRBC_SM_LEAN": "0"},
+            # LDS-staged records read per lane even where every wave holds one
+            # instance (default at nodes % 64 == 0: scalar dispatch)
+            "wi_off": {"HBRBC_SM_WI": "0"}}
 
 
 def test_single_root_scenarios_on_host():
