@@ -519,3 +519,28 @@ def test_local_rounds_run_twice_from_fresh_nodes():
     assert (first, sm.records, sm.ran) == (second, rec1, ran1) == (5, 4 * sm.out_count.numel(),
                                                                    [0, 1, 2, 3, 4])
     assert run_rounds([sm]) == 5 and sm.records == rec1
+
+
+def test_round_flags_raise_distinct_errors():
+    """CPU: the per-round flags the kernels OR into emitted[1] -- bit 0 a node
+    emitted more than max_out records, bit 1 a record kind (or a fake_from
+    node) that the launch's handler set leaves out (hbrbc_sm_args.flags) --
+    raise their own errors in the read-back; a clean quiescent batch returns
+    the round count."""
+    import torch
+
+    from hbbft_amd.rbc_sim import _check_batch
+
+    class _R:
+        max_out = 4
+        records = 0
+
+    ranks = [_R()]
+    ok = torch.tensor([[[5, 0], [3, 0], [0, 0]]], dtype=torch.int32)   # [ranks][rounds][2]
+    assert _check_batch(ranks, ok, 0) == 3 and ranks[0].records == 8
+    with pytest.raises(RuntimeError, match="more than 4 messages"):
+        _check_batch(ranks, torch.tensor([[[5, 1]]], dtype=torch.int32), 0)
+    with pytest.raises(RuntimeError, match="without those handlers"):
+        _check_batch(ranks, torch.tensor([[[5, 2]]], dtype=torch.int32), 0)
+    with pytest.raises(RuntimeError, match="without those handlers"):
+        _check_batch(ranks, torch.tensor([[[5, 3]]], dtype=torch.int32), 0)
