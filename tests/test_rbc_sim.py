@@ -357,12 +357,13 @@ def test_lean_rounds_multi_root_match_host(n, worlds):
 
 
 @pytest.mark.gpu
-def test_lean_round_rejects_injected_records():
+def test_lean_round_rejects_injected_records(monkeypatch):
     """A batch WITH a fake_from node marked HBRBC_SM_NO_FAKE anyway: its Fake
     node reaches a round run without the Fake handler, which reports it
     (emitted[1] bit 1), and the driver raises instead of dropping the
     injection."""
     from hbbft_amd.rbc_sim import SM_NO_FAKE, StateMachineRank, data_plane, run_rounds
+    monkeypatch.delenv("HBRBC_SM_LEAN", raising=False)   # (=0 would run the full set)
     n = 7
     insts = [i for i in make_instances(n, random.Random(3)) if i.fake_from is not None]
     scn = Scenario(n, insts)
