@@ -41,6 +41,18 @@
 #include <cstring>
 #include <type_traits>
 
+// Kernel forms (launch_sm_round picks one per round): where the state and
+// records live -- global (sm_round_kernel), LDS-staged state and records
+// (sm_round_staged_kernel), LDS-staged state with the records read from the
+// all-gathered inbox through the scalar cache (sm_round_grec_kernel, nodes %
+// 64 == 0) -- each at the default register budget or at 4 waves/SIMD (_w4);
+// the handler set LV (Sm::deliver: every handler, or without the Fake / Value
+// handlers for batches marked HBRBC_SM_NO_FAKE); and for the staged form WI,
+// every wave one instance (the record dispatch as scalar branches).  Round 5
+// (DESIGN.md 6c): the smaller handler sets, the scalar dispatch and the
+// pointer-walking cursor took N=128 from 1.07 to 0.76 ms and N=64 from 0.65 to
+// 0.55 ms per run of tools/sm_bench.py.
+
 // Compile-time A/B switches of the one-root round kernel (round 4):
 // HB_SM_CACHE keeps the inbox loop's 32-sender mask word in registers,
 // HB_SM_MERGE takes a sender's Echo and EchoHash in one step.  Measured
