@@ -90,6 +90,10 @@ namespace hbrbc {
 namespace {
 
 constexpr uint32_t kNone = 0xFFu;
+// record header: kind | root << 8 | index << 16 | tamper << 24; bit 7 of the
+// kind byte marks an Echo whose next record is the EchoHash of the same
+// handle_value step (disjoint targets: the receivers merge the two, below)
+constexpr uint32_t kKindMask = 0x7Fu, kPairFlag = 0x80u;
 
 // message kinds (broadcast::Message, message.rs:13-24) + the fake block
 enum { K_VALUE = 0, K_ECHO = 1, K_READY = 2, K_CAN_DECODE = 3, K_ECHO_HASH = 4, K_FAKE = 5 };
@@ -564,7 +568,18 @@ struct Sm {
         send_echo_hash(c);
         const uint32_t m1 = nout, f1 = nfault;
         send_echo_left(c, j, t);
-        if (!overflow) rotate_tail(m0, m1, f0, f1);
+        if (!overflow) {
+            rotate_tail(m0, m1, f0, f1);
+            // flag the Echo that the step's EchoHash now directly follows
+            // (Echo to all but the right nodes, EchoHash to the right ones)
+            for (uint32_t q = m0; q + 1 < nout; ++q) {
+                uint32_t &hq = out[(size_t)q * rec];
+                if ((hq & kKindMask) == K_ECHO && (out[(size_t)(q + 1) * rec] & kKindMask) == K_ECHO_HASH) {
+                    hq |= kPairFlag;
+                    break;
+                }
+            }
+        }
     }
 
     // the ProposeAdversary's injected step: per listed faulty node F (in index
@@ -596,7 +611,7 @@ struct Sm {
     // lanes of a merged step take different kinds (the per-lane kind is only
     // the handler's `full` operand)
     __device__ __forceinline__ void deliver(int s, uint32_t h0, uint32_t k0) {
-        const uint32_t kind = h0 & 0xFFu, c0 = (h0 >> 8) & 0xFFu;
+        const uint32_t kind = h0 & kKindMask, c0 = (h0 >> 8) & 0xFFu;
         const uint32_t j = (h0 >> 16) & 0xFFu, t = (h0 >> 24) & 0xFFu;
         if constexpr (LV == 2) {
             // the round's common kinds first (a switch became a compare tree)
@@ -819,8 +834,6 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
         // (no lane test for s == me: no record targets its own sender, so
         // that lane's bit is clear -- a divergent `continue` cost exec-mask
         // work on every sender)
-        // Echo / EchoHash kinds as a bit set (the merge test below)
-        constexpr uint32_t kEchoKinds = (1u << K_ECHO) | (1u << K_ECHO_HASH);
         // wave-uniform records: the global-records kernel's (scalar loads),
         // and an LDS-staged inbox whose waves each hold one instance (values
         // read per lane, equal in every lane, moved to scalar registers: the
@@ -838,31 +851,25 @@ __device__ __forceinline__ void sm_node(const hbrbc_sm_args &a, int n, int f, in
             in.advance();
             for (uint32_t e = 0; e < cnt; ++e, r += rw) {
                 uint32_t h0 = uni(r[0]);
-                const uint32_t k0 = h0 & 0xFFu;
+                const uint32_t k0 = h0 & kKindMask;
                 bool hit = rbit(r);
-                // An Echo and an EchoHash of the same sender in a row whose
-                // targets do not overlap at this node (handle_value emits
-                // Echo to all but the right nodes, EchoHash to the right
-                // ones): this node handles at most one of them, so both are
-                // taken in one step through the merged handler (a sequential
-                // step is always exact).  In the global-records kernel the
-                // step is taken only when every lane of the wave can take it,
-                // so the record index stays wave-uniform (scalar loads, and
-                // the kind tests are scalar branches).
-                if (HB_SM_MERGE && ((kEchoKinds >> k0) & 1u) && e + 1 < cnt) {
+                // An Echo flagged by its sender (kPairFlag) is followed by the
+                // EchoHash of the same step, whose targets are disjoint from
+                // its own (handle_value: Echo to all but the right nodes,
+                // EchoHash to the right ones): a node handles at most one of
+                // them, so both are taken in one step through the merged
+                // handler (a sequential step is always exact).  The flag is in
+                // the header, so the step is wave-uniform wherever the records
+                // are (round 5: it replaced per-record kind tests and a
+                // wave-wide vote on the two recipient bits).
+                if (HB_SM_MERGE && (h0 & kPairFlag) && e + 1 < cnt) {
                     const uint32_t h1 = uni(r[rw]);
-                    const uint32_t k1 = h1 & 0xFFu;
-                    if (((kEchoKinds >> k1) & 1u) && k1 != k0) {
-                        const bool hit2 = rbit(r + rw);
-                        const bool ok = !(hit && hit2);
-                        if (UNI ? __all(ok) : ok) {
-                            ++e;
-                            r += rw;
-                            if (hit2) {
-                                h0 = h1;
-                                hit = true;
-                            }
-                        }
+                    const bool hit2 = rbit(r + rw);
+                    ++e;
+                    r += rw;
+                    if (hit2) {
+                        h0 = h1;
+                        hit = true;
                     }
                 }
                 if (!hit) continue;
