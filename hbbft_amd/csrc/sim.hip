@@ -49,9 +49,10 @@
 // the handler set LV (Sm::deliver: every handler, or without the Fake / Value
 // handlers for batches marked HBRBC_SM_NO_FAKE); and for the staged form WI,
 // every wave one instance (the record dispatch as scalar branches).  Round 5
-// (DESIGN.md 6c): the smaller handler sets, the scalar dispatch and the
-// pointer-walking cursor took N=128 from 1.07 to 0.76 ms and N=64 from 0.65 to
-// 0.55 ms per run of tools/sm_bench.py.
+// (DESIGN.md 6c): the smaller handler sets, the scalar dispatch, the
+// pointer-walking cursor and sender-flagged Echo / EchoHash pairs took N=128
+// from 1.07 to 0.74 ms and N=64 from 0.65 to 0.53 ms per run of
+// tools/sm_bench.py.
 
 // Compile-time A/B switches of the one-root round kernel (round 4):
 // HB_SM_CACHE keeps the inbox loop's 32-sender mask word in registers,
