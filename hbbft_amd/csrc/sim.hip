@@ -569,7 +569,28 @@ struct Sm {
         send_echo_hash(c);
         const uint32_t m1 = nout, f1 = nfault;
         send_echo_left(c, j, t);
-        if (!overflow) {
+        const uint32_t fl = nfault < a.max_faults ? nfault : a.max_faults;
+        if (!overflow && m1 == m0 + 1 && nout == m1 + 1 && (f1 == f0 || fl <= f1)) {
+            // the common step -- one EchoHash record, one Echo record, no
+            // fault to move: both records are read at once and written back
+            // swapped, the Echo flagged (one load round trip instead of the
+            // rotation's one per word, and no second pass for the flag)
+            uint32_t ea[9], eb[9];
+#pragma unroll
+            for (int w = 0; w < 9; ++w) {
+                const int ww = w < rec ? w : rec - 1;   // rec <= 9 (n <= 256)
+                ea[w] = out[(size_t)m0 * rec + ww];
+                eb[w] = out[(size_t)m1 * rec + ww];
+            }
+            if ((eb[0] & kKindMask) == K_ECHO && (ea[0] & kKindMask) == K_ECHO_HASH) eb[0] |= kPairFlag;
+#pragma unroll
+            for (int w = 0; w < 9; ++w) {
+                if (w < rec) {
+                    out[(size_t)m0 * rec + w] = eb[w];
+                    out[(size_t)m1 * rec + w] = ea[w];
+                }
+            }
+        } else if (!overflow) {
             rotate_tail(m0, m1, f0, f1);
             // flag the Echo that the step's EchoHash now directly follows
             // (Echo to all but the right nodes, EchoHash to the right ones)
