@@ -50,9 +50,9 @@
 // handlers for batches marked HBRBC_SM_NO_FAKE); and for the staged form WI,
 // every wave one instance (the record dispatch as scalar branches).  Round 5
 // (DESIGN.md 6c): the smaller handler sets, the scalar dispatch, the
-// pointer-walking cursor and sender-flagged Echo / EchoHash pairs took N=128
-// from 1.07 to 0.74 ms and N=64 from 0.65 to 0.53 ms per run of
-// tools/sm_bench.py.
+// pointer-walking cursor, sender-flagged Echo / EchoHash pairs and vote-
+// guarded rare steps took N=128 from 1.07 to 0.73 ms and N=64 from 0.65 to
+// 0.52 ms per run of tools/sm_bench.py.
 
 // Compile-time A/B switches of the one-root round kernel (round 4):
 // HB_SM_CACHE keeps the inbox loop's 32-sender mask word in registers,
@@ -95,6 +95,19 @@ constexpr uint32_t kNone = 0xFFu;
 // kind byte marks an Echo whose next record is the EchoHash of the same
 // handle_value step (disjoint targets: the receivers merge the two, below)
 constexpr uint32_t kKindMask = 0x7Fu, kPairFlag = 0x80u;
+
+// A rare lane-divergent step behind a wave-wide test: HB_RARE(c) { if (c) ... }
+// skips with one vote and a uniform branch where a plain divergent `if` costs
+// an exec-mask save, a branch and a restore on every record (HB_SM_RARE=0:
+// plain ifs, A/B).
+#ifndef HB_SM_RARE
+#define HB_SM_RARE 1
+#endif
+#if HB_SM_RARE
+#define HB_RARE(c) if (__builtin_expect(__any(c), 0))
+#else
+#define HB_RARE(c) if (true)
+#endif
 
 // message kinds (broadcast::Message, message.rs:13-24) + the fake block
 enum { K_VALUE = 0, K_ECHO = 1, K_READY = 2, K_CAN_DECODE = 3, K_ECHO_HASH = 4, K_FAKE = 5 };
@@ -367,7 +380,12 @@ struct Sm {
 
     // -- handlers (broadcast.rs) --------------------------------------------
     __device__ __forceinline__ void compute_output(uint32_t c) {   // 526-558
-        if ((FLAGS() & FL_DECIDED) || CR(c) <= 2 * f || CF(c) < k) return;
+        const bool fire = !(FLAGS() & FL_DECIDED) && CR(c) > 2 * f && CF(c) >= k;
+        HB_RARE(fire) {
+            if (fire) output_now(c);
+        }
+    }
+    __device__ __forceinline__ void output_now(uint32_t c) {
         if (dok[c]) {
             FLAGS() |= FL_DECIDED;
             a.output_root[inst * a.nodes + (me - a.node_lo)] = (uint8_t)c;
@@ -486,7 +504,9 @@ struct Sm {
             flt = any && c != 0u;
             fk = F_MULTIPLE_ECHO_HASHES;
         }
-        if (__builtin_expect(flt, 0)) fault(s, fk);
+        HB_RARE(flt) {
+            if (flt) fault(s, fk);
+        }
         const bool go = !stop;
         r_ce += (go && !any) ? 1 : 0;
         r_cf += (go && full) ? 1 : 0;
@@ -499,8 +519,12 @@ struct Sm {
         const bool cd = go && full && !(r_flags & (1u << FL_CAN_DECODE_SHIFT)) && r_cf >= (uint32_t)k;
         const bool rd_ok = go && !(r_flags & FL_READY_SENT) && r_ce >= (uint32_t)(n - f);
         const bool co = go && (rd_ok ? full : (!full || (r_flags & FL_READY_SENT)));
-        if (__builtin_expect(cd, 0)) send_can_decode(c);
-        if (__builtin_expect(rd_ok, 0)) send_ready(c);
+        HB_RARE(cd) {
+            if (cd) send_can_decode(c);
+        }
+        HB_RARE(rd_ok) {
+            if (rd_ok) send_ready(c);
+        }
         if (co) compute_output(c);
     }
     __device__ __forceinline__ void handle_echo(int s, uint32_t c, uint32_t j, uint32_t t) {
@@ -686,14 +710,25 @@ __device__ __forceinline__ void Sm<ONE>::handle_ready_core(int s, uint32_t c, bo
         const uint32_t b = 1u << (s & 31);
         uint4 m4 = em_get(w);
         const bool had = m4.w & b;
-        if (__builtin_expect(had && c != 0u, 0)) fault(s, F_MULTIPLE_READYS);
+        HB_RARE(had && c != 0u) {
+            if (had && c != 0u) fault(s, F_MULTIPLE_READYS);
+        }
         const bool go = !had;
         m4.w |= go ? b : 0u;
         em_put(w, m4);
         r_cr += go ? 1 : 0;
-        if (__builtin_expect(go && may_send && r_cr == f + 1 && !(r_flags & FL_READY_SENT), 0))
-            send_ready(c);
-        if (__builtin_expect(go && r_cr == 2 * f + 1, 0)) send_echo_remaining(c);
+        {
+            const bool sr = go && may_send && r_cr == f + 1 && !(r_flags & FL_READY_SENT);
+            HB_RARE(sr) {
+                if (sr) send_ready(c);
+            }
+        }
+        {
+            const bool ser = go && r_cr == 2 * f + 1;   // (after send_ready moved the count)
+            HB_RARE(ser) {
+                if (ser) send_echo_remaining(c);
+            }
+        }
         if (go) compute_output(c);
         return;
     }
