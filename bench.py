@@ -91,6 +91,18 @@ def parse():
     ap.add_argument("--no-sm-overlap", action="store_true",
                     help="validator mode on one rank: run each step's state machine after its "
                          "decode instead of beside the next step's data plane")
+    ap.add_argument("--sm-overlap", action="store_true",
+                    help="validator mode with >1 rank: run the overlapped schedule (state machine "
+                         "on a side stream with its own process group) instead of the serial one")
+    ap.add_argument("--pg-timeout", type=float, default=120.0,
+                    help="seconds: timeout of every process group (a stuck collective ends the "
+                         "run instead of running into the driver's limit)")
+    ap.add_argument("--phase-budget", type=float, default=100.0,
+                    help="seconds: a validator-sharded object still running after this long is "
+                         "recorded as an error and the line is printed without it")
+    ap.add_argument("--detail", default="",
+                    help="write the full per-object record (stage tables, per-rank exchange "
+                         "records, footprints, prose) to this JSON file; stdout gets the compact line")
     ap.add_argument("--vpipes", type=int, default=int(os.environ.get("HBRBC_BENCH_VPIPES", "2")),
                     help="one rank: step pipelines on their own HIP streams, step i on pipe "
                          "i %% vpipes (each with its own buffers and state machines)")
@@ -367,6 +379,9 @@ def cpu_baseline(args, n, f, plen, n_erase, config):
     return {"value": sample * plen / med / 1e9, "unit": "GB/s", "cores": threads,
             "kind": "port", "reps": args.cpu_reps, "host_cpus": os.cpu_count(),
             "affinity_cpus": cpus, "cgroup_cpu_quota": quota,
+            "sample_short": "%d instances of %s through oracle/rbc_oracle.c (the reference's "
+                            "algorithm), %d threads, median of %d reps, %d/%d decoded ok"
+                            % (sample, config, threads, args.cpu_reps, ok, sample),
             "single_core": {"value": s1 * plen / med1 / 1e9, "unit": "GB/s", "cores": 1,
                             "sample": "%d instances, median of %d" % (s1, args.cpu_reps)},
             "sample": "%d instances of %s (N=%d, %d B payload, %s) through the same pipeline in "
@@ -435,6 +450,9 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
     # writes the payload from rebuilt rows (the decode never runs on rows
     # that still hold the right bytes).  The row ids of every pattern (and
     # sub-batch) are built here, outside the timed region.
+    # The fill simulates transport, not reference work: its HIP-event spans
+    # (same stream, between the validate and the decode) are taken out of the
+    # timed region's wall time for `value`; `value_incl_erase` keeps them.
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
     erase_spans = []
 
@@ -445,9 +463,9 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         e0.record()
         subs_rb[q].drop_rows(slab[sl], pool[i % len(pool)][sl], 0xA5)   # hbrbc_drop_rows
         e1.record()
-        if timing_erase[0]:
-            erase_spans.append((e0, e1))
-    timing_erase = [False]
+        if timing_erase[0] is not None:
+            timing_erase[0].append((e0, e1))
+    timing_erase = [None]
 
     main = torch.cuda.current_stream(dev)
     subs = []
@@ -514,7 +532,7 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
     for sb in subs_rb:
         sb.profile(True)
         sb.profile_reset()
-    timing_erase[0] = True
+    timing_erase[0] = erase_spans
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -525,10 +543,16 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timing_erase[0] = False
+    timing_erase[0] = None
     for sb in subs_rb:
         sb.profile(False)
-    elapsed = max_over_ranks(elapsed, world, dev)
+    erase_s = sum(a.elapsed_time(b) for a, b in erase_spans) / 1e3
+    # one stream: the erase spans are serial with the reference work and come
+    # out of the wall time; sub-batches on several streams overlap them, so
+    # nothing is subtracted there
+    work = elapsed - (erase_s if nsub == 1 else 0.0)
+    elapsed_all = max_over_ranks(elapsed, world, dev)
+    elapsed = max_over_ranks(work, world, dev)
     verified = False
     if not args.no_verify:
         check("last timed step")   # the outputs of the last timed step, from garbage rows
@@ -538,13 +562,13 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         for st_name, (ms, cnt) in sb.profile_read().items():
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
-    stages["erase"] = (sum(a.elapsed_time(b) for a, b in erase_spans), len(erase_spans))
+    stages["erase"] = (erase_s * 1e3, len(erase_spans))
     value = float(count) * plen * world * args.steps / elapsed / 1e9
     lr = None
     if leaf_reuse and not args.no_leaf_reuse and nsub == 1 and erase == "f":
         lr = run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests,
                             ndig, ok, out, plen_out, status, S, n, f, world, dev,
-                            erase_rows)
+                            erase_rows, timing_erase)
     em = None
     if encode_merkle:
         em = run_encode_merkle(args, rb, payloads, plen, slab, nodes, digests, ndig, S, world,
@@ -555,6 +579,8 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
     roof["unframe_fused"] = rb.unframe_fused(S, out.stride(0))
     r = {
         "value": value, "unit": "GB/s", "ms_per_step": elapsed / args.steps * 1e3,
+        "value_incl_erase": float(count) * plen * world * args.steps / elapsed_all / 1e9,
+        "ms_per_step_incl_erase": elapsed_all / args.steps * 1e3,
         "roofline": roof,
         "stages_ms_per_step": {s: stages[s][0] / args.steps for s in stages},
         "config": {"workload": "%s: N=%d f=%d (%d+%d shards), %d B payloads, %d instances/GPU, "
@@ -566,9 +592,10 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         "n_erase": n_erase, "f": f, "leaf_reuse": lr,
         "verified_last_timed_step": verified,
         "decode_input": ("every step overwrites the %d erased rows of each instance with garbage "
-                         "after validation (stage `erase`), so each timed decode rebuilds them; "
-                         "the last timed step's payloads and decode trees are checked"
-                         % n_erase),
+                         "after validation (stage `erase`, transport: its HIP-event time is "
+                         "outside `value`, inside `value_incl_erase`), so each timed decode "
+                         "rebuilds them; the last timed step's payloads and decode trees are "
+                         "checked" % n_erase),
     }
     if em is not None:
         r["encode_merkle"] = em
@@ -576,7 +603,7 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
 
 
 def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests, ndig,
-                   ok, out, plen_out, status, S, n, f, world, dev, erase_rows):
+                   ok, out, plen_out, status, S, n, f, world, dev, erase_rows, timing_erase):
     """Labelled variant of the instance step, NOT the headline: validate
     writes each validated row's Merkle leaf into the decode tree
     (hbrbc_validate_rows leaf_out), and the decode hashes only the rows the
@@ -621,6 +648,8 @@ def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, d
         out.fill_(0x5A)
     rb.profile(True)
     rb.profile_reset()
+    spans = []
+    timing_erase[0] = spans
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -631,12 +660,17 @@ def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, d
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    wall = time.perf_counter() - t0
+    timing_erase[0] = None
+    # like the headline: the erase fill (transport) is outside `value`
+    erase_s = sum(a.elapsed_time(b) for a, b in spans) / 1e3
+    elapsed = max_over_ranks(wall - erase_s, world, dev)
     rb.profile(False)
     if not args.no_verify:
         check("last timed step")
         verified = True
     stages = {k_: v_[0] / args.steps for k_, v_ in rb.profile_read().items()}
+    stages["erase"] = erase_s * 1e3 / args.steps
     bl = (S + 1 + 135) // 136          # Keccak blocks per leaf (SHA3-256 rate 136)
     depth = max(1, (n - 1).bit_length())
     tree = n * bl + (n - 1)
@@ -716,9 +750,12 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
                                    pipelined_step)
 
     # the state machine of step i on a side stream beside the data plane of
-    # step i + 1 (two state-machine slots), at every world size; at world > 1
-    # its per-round all-gathers run over a process group of their own
-    overlap = not args.no_sm_overlap
+    # step i + 1 (two state-machine slots).  One rank: the default.  More
+    # ranks: opt-in (--sm-overlap; its per-round all-gathers then run over a
+    # process group of their own, concurrently with the data plane's
+    # collectives, which has never run on RCCL); the default there is the
+    # serial schedule -- one communicator, one stream, sub-batches pipelined
+    overlap = not args.no_sm_overlap and (world == 1 or args.sm_overlap)
     # serial schedule at world > 1: sub-batches with every exchange in flight
     nsub = max(1, min(args.vsubs, count)) if world > 1 and not overlap else 1
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
@@ -847,6 +884,8 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     return {
         "value": value, "unit": "GB/s", "ms_per_step": elapsed / args.steps * 1e3,
         "scaling": "weak in proposals (every rank decodes all world x count instances)",
+        "schedule": "%s, %d pipe(s), %d sub-batch(es)" % ("overlapped" if overlap else "serial",
+                                                          npipe, nsub),
         "scaling_model": ("every node outputs every broadcast, so each rank decodes all world x "
                           "count instances while its proposals stay fixed: time(G) ~ count x "
                           "(encode + tree + Value validate) + G x count x (Echo validate + decode) "
@@ -892,6 +931,7 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
 
 
 _SM_EX = []
+PG_TIMEOUT = [None]    # datetime.timedelta of every process group (main() sets it)
 
 
 def sm_exchange():
@@ -903,7 +943,8 @@ def sm_exchange():
 
     from hbbft_amd.sharded import DistExchange
     if not _SM_EX:
-        _SM_EX.append(DistExchange(dist.new_group(list(range(dist.get_world_size())))))
+        _SM_EX.append(DistExchange(dist.new_group(list(range(dist.get_world_size())),
+                                                  timeout=PG_TIMEOUT[0])))
     return _SM_EX[0]
 
 
@@ -1036,7 +1077,7 @@ def run_threshold(args, rank, world, dev):
         ok = step()
     torch.cuda.synchronize(dev)
     if not torch.equal(ok.cpu(), expect):
-        raise SystemExit("bench f4: check outcomes differ from the fixtures")
+        raise AssertionError("bench f4: check outcomes differ from the fixtures")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -1093,10 +1134,231 @@ def run_threshold(args, rank, world, dev):
                     "(one share in eight tampered); outcomes verified exactly",
             "roofline": roof}
 
+# ------------------------------------------------------------ the line --
+LINE_CAP = 8000   # bytes: the driver keeps the last ~8 KB of stdout
+
+
+def _sig(x, d=4):
+    """Round floats to d significant digits (the compact line)."""
+    if isinstance(x, float):
+        if x != x or x in (float("inf"), float("-inf")) or x == 0.0:
+            return x
+        from math import floor, log10
+        return round(x, max(0, d - 1 - int(floor(log10(abs(x))))))
+    if isinstance(x, dict):
+        return {k: _sig(v, d) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_sig(v, d) for v in x]
+    return x
+
+
+def _get(d, *path):
+    for p_ in path:
+        if not isinstance(d, dict) or p_ not in d:
+            return None
+        d = d[p_]
+    return d
+
+
+def _compact_obj(o, extra=()):
+    """One secondary object: value, time, workload, roofline fraction and the
+    verification flag (errors pass through, truncated)."""
+    if o is None:
+        return None
+    if "error" in o:
+        return {"error": str(o["error"])[:300]}
+    r = {"value": o.get("value"), "unit": o.get("unit"), "ms_per_step": o.get("ms_per_step"),
+         "workload": _get(o, "config", "workload"), "roofline_frac": _get(o, "roofline", "frac"),
+         "roofline_kernel": _get(o, "roofline", "kernel"),
+         "verified_last_timed_step": o.get("verified_last_timed_step")}
+    for key, path in extra:
+        r[key] = _get(o, *path)
+    return {k: v for k, v in r.items() if v is not None}
+
+
+def compact_line(full, detail_path=None):
+    """The line rank 0 prints: the contract's fields, the dominant kernel's
+    roofline and the CPU baseline in full, and per secondary object only its
+    rate, time, workload, roofline fraction and verification flag; everything
+    else (stage tables, per-rank records, footprints, prose) is in the
+    --detail file.  At most LINE_CAP bytes."""
+    keep = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data"]
+    line = {k: full.get(k) for k in keep}
+    cfg = full.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "n", "f", "payload_bytes", "shard_len",
+                                          "instances_per_gpu", "global_batch", "parallelism",
+                                          "proposals_per_gpu") if k in cfg}
+    ro = full.get("roofline")
+    if ro:
+        line["roofline"] = {
+            "kernel": ro.get("kernel"), "bound": ro.get("bound"), "achieved": ro.get("achieved"),
+            "peak": ro.get("peak"), "unit": ro.get("unit"), "frac": ro.get("frac"),
+            "traffic": ro.get("traffic"), "launch_ms": ro.get("launch_ms"),
+            "hbm_frac": _get(ro, "hbm", "frac"), "pipeline_hbm_frac": ro.get("pipeline_hbm_frac"),
+            "profiled_frac": _get(ro, "profiled", "frac"),
+            "frac_of_sustained_clock_ceiling": _get(ro, "sustained_clock", "frac")}
+    else:
+        line["roofline"] = None
+    cb = full.get("cpu_baseline")
+    line["cpu_baseline"] = None if cb is None else {
+        "value": cb.get("value"), "unit": cb.get("unit"), "cores": cb.get("cores"),
+        "kind": cb.get("kind"), "single_core": _get(cb, "single_core", "value"),
+        "sample": cb.get("sample_short", cb.get("sample", ""))[:200]}
+    if "cpu_baseline_note" in full:
+        line["cpu_baseline_note"] = full["cpu_baseline_note"]
+    for k in ("value_incl_erase", "stages_ms_per_step"):
+        if k in full:
+            line[k] = full[k]
+    objs = [("leaf_reuse", ()),
+            ("cfg2", (("encode_merkle", ("encode_merkle", "value")),
+                      ("encode_merkle_ms", ("encode_merkle", "ms_per_step")))),
+            ("cfg5", ()),
+            ("threshold_decrypt", (("cpu_baseline", ("cpu_baseline", "value")),
+                                   ("cpu_cores", ("cpu_baseline", "cores")))),
+            ("validators", (("exchange_ms", ("exchange", "ms_per_step")),
+                            ("schedule", ("schedule",)))),
+            ("validators_cfg4", (("exchange_ms", ("exchange", "ms_per_step")),
+                                 ("schedule", ("schedule",))))]
+    for key, extra in objs:
+        if key in full:
+            line[key] = _compact_obj(full[key], extra)
+    line["detail"] = detail_path
+    line = _sig(line)
+    # hard cap: drop the optional fields, largest first, until the line fits
+    for drop in ("stages_ms_per_step", "leaf_reuse", "data"):
+        if len(json.dumps(line)) <= LINE_CAP:
+            break
+        line.pop(drop, None)
+    assert len(json.dumps(line)) <= LINE_CAP, len(json.dumps(line))
+    return line
+
+
+def assemble(args, world, res, cpu):
+    """The full record (what --detail writes) from the phase results."""
+    head = res.get("head")
+    vobj = res.get("validators")
+    if head is not None and "error" not in head:
+        line = {
+            "metric": METRIC, "value": head["value"], "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (counter-PRNG payloads and f-erasure patterns generated in "
+                    "HBM, identical to the CPU baseline's)",
+            "config": head["config"], "roofline": head["roofline"], "cpu_baseline": cpu,
+            "stages_ms_per_step": head["stages_ms_per_step"],
+        }
+        for k in ("value_incl_erase", "ms_per_step_incl_erase", "decode_input"):
+            if k in head:
+                line[k] = head[k]
+        if head.get("leaf_reuse") is not None:
+            line["leaf_reuse"] = head["leaf_reuse"]
+        if cpu is None and world > 1:
+            line["cpu_baseline_note"] = ("measured on rank 0 of the N=1 run only (bench "
+                                         "contract); see that line's cpu_baseline")
+    elif vobj is not None and "error" not in vobj and args.mode == "validators":
+        line = {
+            "metric": METRIC, "value": vobj["value"], "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": vobj["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (counter-PRNG payloads generated in HBM)",
+            "config": vobj["config"], "roofline": None, "cpu_baseline": cpu,
+        }
+    else:
+        line = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                "config": {}, "roofline": None, "cpu_baseline": cpu,
+                "error": str((head or vobj or {}).get("error", "no headline"))[:300]}
+    for key in ("validators", "validators_cfg4", "cfg2", "cfg5", "threshold_decrypt"):
+        if res.get(key) is not None:
+            line[key] = res[key]
+    return line
+
+
+class Phases:
+    """Runs the bench's objects in order on every rank and keeps the line.
+
+    Secondary objects are guarded: an exception becomes {"error": ...}; at
+    world > 1 the ranks then agree (MIN all-reduce of a success flag) so that
+    none runs the next object's collectives alone.  Every secondary object
+    runs under a deadline (a rank that failed before a collective its peers
+    are waiting in, or an RCCL schedule that stalls): if it is still running
+    after `budget` seconds, rank 0 prints the line with what has been
+    measured and that object as an error, and every rank ends its process
+    (os._exit) -- the headline, measured first, is never lost."""
+
+    def __init__(self, world, rank, dev, budget, emit, backend_cpu):
+        import threading
+        self.world, self.rank, self.dev, self.budget = world, rank, dev, budget
+        self.emit = emit                # emit(results) -> prints the line on rank 0
+        self.backend_cpu = backend_cpu  # gloo: the flag tensor lives on the host
+        self.res = {}
+        self.lock = threading.Lock()
+        self.fired = False
+
+    def agree(self, ok):
+        if self.world == 1:
+            return ok
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                         device="cpu" if self.backend_cpu else self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def _expire(self, name):
+        with self.lock:
+            if self.fired is not None:   # the phase finished in time (or already fired)
+                return
+            self.fired = True
+            self.res[name] = {"error": "timeout: still running after %.0f s (phase budget); "
+                                       "the process ended here" % self.budget}
+            try:
+                self.emit(self.res)
+            finally:
+                sys.stdout.flush()
+                sys.stderr.write("bench: %s exceeded its %.0f s budget; line printed, exiting\n"
+                                 % (name, self.budget))
+                sys.stderr.flush()
+                os._exit(0)
+
+    def run(self, name, fn, required=False, watch=False):
+        import threading
+        timer = None
+        if watch and self.budget > 0:
+            with self.lock:
+                self.fired = None
+            timer = threading.Timer(self.budget, self._expire, args=(name,))
+            timer.daemon = True
+            timer.start()
+        ok, val = True, None
+        try:
+            val = fn()
+        except Exception as e:  # noqa: BLE001
+            if required:
+                raise
+            ok = False
+            val = {"error": "%s: %s" % (type(e).__name__, e)}
+            print("bench: %s failed: %r" % (name, e), file=sys.stderr)
+        finally:
+            if timer is not None:
+                with self.lock:
+                    if self.fired is None:
+                        self.fired = False
+                timer.cancel()
+        if not self.agree(ok) and ok:
+            val = {"error": "failed on another rank (this rank completed it)"}
+        self.res[name] = val
+        return val
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn(args)
+    import datetime
+
     import torch
     import torch.distributed as dist
 
@@ -1112,126 +1374,118 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    PG_TIMEOUT[0] = datetime.timedelta(seconds=args.pg_timeout)
     if world > 1:
         if rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=PG_TIMEOUT[0])
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=PG_TIMEOUT[0])
         assert dist.get_world_size() == args.gpus
         assert rehearse or dist.get_backend() == "nccl", "multi-GPU runs use RCCL"
+    return run_bench(args, world, rank, dev, local, real_phases(args, world, rank, dev, local),
+                     backend_cpu=rehearse)
 
+
+def real_phases(args, world, rank, dev, local):
+    """name -> callable of every object of the line, in the order they run:
+    the instance-mode objects (headline, cfg2, cfg5, f4: no data-path
+    collective) first, then the validator-sharded ones (RCCL exchanges)."""
+    import torch
     n, plen, count, erase, vcount = CONFIGS[args.config]
     count = args.count or count
     vcount = args.vcount or vcount
-    head = vobj = None
-    if args.mode in ("instances", "both"):
-        head = run_instances(args, n, plen, count, erase, rank, world, dev, local,
-                             encode_merkle=args.config == "cfg2")
-    if args.mode in ("validators", "both"):
-        torch.cuda.empty_cache()
-        if head is None:
-            vobj = run_validators(args, n, plen, vcount, rank, world, dev, local)
-        else:
-            # the headline is measured: a failure of the (secondary) validator
-            # simulation is reported in the line instead of losing it
-            try:
-                vobj = run_validators(args, n, plen, vcount, rank, world, dev, local)
-            except Exception as e:  # noqa: BLE001
-                vobj = {"error": "%s: %s" % (type(e).__name__, e)}
-                print("bench: validator-sharded run failed: %r" % (e,), file=sys.stderr)
+    both = args.mode == "both" and args.config == "cfg3"
+    ph = []
 
-    # cfg4 (N=128, validators sharded over the ranks, RCCL all-to-all + all-gather)
-    # rides along the default cfg3 line so the driver's multi-GPU runs measure it
-    v4 = None
-    if args.mode == "both" and args.config == "cfg3" and not args.no_cfg4:
-        torch.cuda.empty_cache()
-        n4, plen4, _, _, vcount4 = CONFIGS["cfg4"]
-        try:
-            v4 = run_validators(args, n4, plen4, args.vcount or vcount4, rank, world, dev, local,
-                                config="cfg4")
-        except Exception as e:  # noqa: BLE001  (secondary object: keep the headline line)
-            v4 = {"error": "%s: %s" % (type(e).__name__, e)}
-            print("bench: cfg4 validator-sharded run failed: %r" % (e,), file=sys.stderr)
-
-    # BASELINE's other GPU configs ride along the default cfg3 line, instance-
-    # sharded over the ranks like the headline, so the driver's 1- and
-    # 8-GPU runs measure them: cfg2 (N=16, 1 MiB x 4096, with its own
-    # encode+Merkle metric) and cfg5 (N=250, 4 MiB, worst-case decode)
-    riders = {}
-    if args.mode == "both" and args.config == "cfg3" and not args.no_riders:
-        for cfg in ("cfg2", "cfg5"):
+    def fresh(fn):
+        def run():
             torch.cuda.empty_cache()
+            return fn()
+        return run
+    if args.mode in ("instances", "both"):
+        ph.append(("head", lambda: run_instances(args, n, plen, count, erase, rank, world, dev,
+                                                 local, encode_merkle=args.config == "cfg2")))
+    if both and not args.no_riders:
+        # BASELINE's other GPU configs, instance-sharded over the ranks like the
+        # headline: cfg2 (N=16, 1 MiB x 4096, with its own encode+Merkle
+        # metric) and cfg5 (N=250, 4 MiB, worst-case decode)
+        for cfg in ("cfg2", "cfg5"):
             n_, plen_, cnt_, er_, _ = CONFIGS[cfg]
-            try:
-                riders[cfg] = run_instances(args, n_, plen_, args.rider_count or cnt_, er_, rank,
-                                            world, dev, local,
-                                            config=cfg, streams=1, leaf_reuse=False,
-                                            encode_merkle=cfg == "cfg2")
-            except Exception as e:  # noqa: BLE001  (secondary object: keep the headline line)
-                riders[cfg] = {"error": "%s: %s" % (type(e).__name__, e)}
-                print("bench: %s instance run failed: %r" % (cfg, e), file=sys.stderr)
-
-    f4 = None
+            ph.append((cfg, fresh(lambda n_=n_, plen_=plen_, cnt_=cnt_, er_=er_, cfg=cfg:
+                                  run_instances(args, n_, plen_, args.rider_count or cnt_, er_,
+                                                rank, world, dev, local, config=cfg, streams=1,
+                                                leaf_reuse=False, encode_merkle=cfg == "cfg2"))))
     if args.f4_checks > 0:
-        torch.cuda.empty_cache()
-        try:
-            f4 = run_threshold(args, rank, world, dev)
-        except SystemExit:
-            raise
-        except Exception as e:  # noqa: BLE001  (secondary leg: keep the headline line)
-            f4 = {"error": "%s: %s" % (type(e).__name__, e)}
-            print("bench: f4 leg failed: %r" % (e,), file=sys.stderr)
-        if rank == 0 and world == 1 and not args.no_cpu and "error" not in f4:
-            gold = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))
-            pool = [{"a": s["share"], "b": g["hash"], "c": s["pk"], "d": g["w"],
-                     "expect": s["expect"]} for g in gold["bench_groups"] for s in g["shares"][:8]]
-            f4["cpu_baseline"] = f4_cpu_baseline(pool, 3)
+        ph.append(("threshold_decrypt", fresh(lambda: run_threshold(args, rank, world, dev))))
+    if args.mode in ("validators", "both"):
+        ph.append(("validators", fresh(lambda: run_validators(args, n, plen, vcount, rank, world,
+                                                              dev, local))))
+    if both and not args.no_cfg4:
+        # cfg4 (N=128, validators sharded over the ranks, RCCL all-to-all + all-gather)
+        n4, plen4, _, _, vcount4 = CONFIGS["cfg4"]
+        ph.append(("validators_cfg4", fresh(lambda: run_validators(
+            args, n4, plen4, args.vcount or vcount4, rank, world, dev, local, config="cfg4"))))
+    return ph
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        f = (n - 1) // 3
-        cpu = cpu_baseline(args, n, f, plen, f if erase == "f" else 2 * f, args.config)
 
-    if rank == 0:
-        if head is not None:
-            line = {
-                "metric": METRIC, "value": head["value"], "unit": "GB/s", "n_gpus": world,
-                "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-                "data": "synthetic (counter-PRNG payloads and f-erasure patterns generated in "
-                        "HBM, identical to the CPU baseline's)",
-                "config": head["config"], "roofline": head["roofline"], "cpu_baseline": cpu,
-                "stages_ms_per_step": head["stages_ms_per_step"],
-            }
-            if head.get("leaf_reuse") is not None:
-                line["leaf_reuse"] = head["leaf_reuse"]
-            if cpu is None and world > 1:
-                line["cpu_baseline_note"] = ("measured on rank 0 of the N=1 run only (bench "
-                                             "contract); see that line's cpu_baseline")
-            if vobj is not None:
-                if cpu is not None and "error" not in vobj:
-                    vobj["cpu_baseline"] = dict(cpu, note="the same per-instance pipeline; the "
-                                                "CPU leg decodes each instance once")
-                line["validators"] = vobj
-            if v4 is not None:
-                line["validators_cfg4"] = v4
-            for cfg, obj in riders.items():
-                line[cfg] = obj
-            if f4 is not None:
-                line["threshold_decrypt"] = f4
-        else:
-            line = {
-                "metric": METRIC, "value": vobj["value"], "unit": "GB/s", "n_gpus": world,
-                "steps": args.steps, "warmup": args.warmup, "ms_per_step": vobj["ms_per_step"],
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-                "data": "synthetic (counter-PRNG payloads generated in HBM)",
-                "config": vobj["config"], "roofline": None, "cpu_baseline": cpu,
-                "validators": vobj,
-            }
-        print(json.dumps(line), flush=True)
+WATCHED = ("validators", "validators_cfg4")   # CPU baselines are taken before these
+
+
+def run_bench(args, world, rank, dev, local, phases, backend_cpu=False, cpu_fn=None):
+    """Run the phases in order (instance objects first, validator-sharded
+    last, each watched), take the CPU baselines on rank 0 of a one-rank run
+    before the watched phases, and print one compact line on rank 0."""
+    n, plen, count, erase, vcount = CONFIGS[args.config]
+    state = {"cpu": None}
+
+    def emit(res):
+        if rank != 0:
+            return
+        full = assemble(args, world, res, state["cpu"])
+        if args.detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+                with open(args.detail, "w") as fh:
+                    json.dump(full, fh, indent=1, default=str)
+            except OSError as e:
+                print("bench: --detail not written: %r" % (e,), file=sys.stderr)
+        print(json.dumps(compact_line(full, args.detail or None)), flush=True)
+
+    P = Phases(world, rank, dev, args.phase_budget, emit, backend_cpu)
+    headline = args.mode in ("instances", "both") and "head" or "validators"
+    cpu_done = False
+    for name, fn in phases:
+        if name in WATCHED and not cpu_done:
+            state["cpu"] = cpu_fn() if cpu_fn else take_cpu_baselines(args, rank, world, P.res,
+                                                                        n, plen, erase)
+            cpu_done = True
+        P.run(name, fn, required=name == headline, watch=name != headline)
+    if not cpu_done:
+        state["cpu"] = cpu_fn() if cpu_fn else take_cpu_baselines(args, rank, world, P.res, n,
+                                                                    plen, erase)
     if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    emit(P.res)
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
     return 0
+
+
+def take_cpu_baselines(args, rank, world, res, n, plen, erase):
+    """Rank 0 of a one-rank run: the pipeline's CPU baseline, and the f4
+    leg's (added to its object)."""
+    if rank != 0 or world != 1 or args.no_cpu:
+        return None
+    f4 = res.get("threshold_decrypt")
+    if f4 is not None and "error" not in f4:
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "bls_vectors.json")))
+        pool = [{"a": s["share"], "b": g["hash"], "c": s["pk"], "d": g["w"],
+                 "expect": s["expect"]} for g in gold["bench_groups"] for s in g["shares"][:8]]
+        f4["cpu_baseline"] = f4_cpu_baseline(pool, 3)
+    f = (n - 1) // 3
+    return cpu_baseline(args, n, f, plen, f if erase == "f" else 2 * f, args.config)
 
 
 if __name__ == "__main__":

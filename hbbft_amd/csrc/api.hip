@@ -1135,7 +1135,7 @@ int decode_rows(hbrbc_ctx *c, uint8_t *shards, size_t shard_len, const RowMap &r
 extern "C" {
 
 const char *hbrbc_last_error(void) { return g_err.c_str(); }
-const char *hbrbc_version(void) { return "hbrbc 0.2.0 gfx950"; }
+// hbrbc_version() lives in version.cpp (built with the source hash)
 
 int hbrbc_coding_new(size_t data_shards, size_t parity_shards, int device, hbrbc_ctx **out) {
     if (!out) return fail(HBRBC_E_INVALID_ARG, "out is null");

@@ -82,7 +82,8 @@ typedef struct hbrbc_ctx hbrbc_ctx;
 
 /* Message of the last failing call on this thread (static storage). */
 const char *hbrbc_last_error(void);
-/* Library version string ("hbrbc <semver> gfx950"). */
+/* Library version string ("hbrbc <semver> gfx950 src=<hash>"; the hash is
+ * hbbft_amd/srchash.py over the sources the library was built from). */
 const char *hbrbc_version(void);
 
 /* ---- context = one `Coding` (broadcast.rs:639-655) --------------------- */

@@ -50,6 +50,18 @@ def test_host_helpers_match_oracle():
     assert [L.hbrbc_stage_name(i).decode() for i in range(9)] == hb.STAGES
 
 
+def test_library_built_from_this_tree():
+    """Provenance: hbrbc_version() carries the hash of the sources the library
+    was compiled from (hbbft_amd/srchash.py via the Makefile); it must be the
+    hash of the sources in this tree."""
+    from hbbft_amd.srchash import source_hash, source_files
+    v = hb.lib().hbrbc_version().decode()
+    assert v.startswith("hbrbc ") and " gfx950 " in v
+    assert v.endswith("src=" + source_hash()), (v, source_hash())
+    files = source_files()
+    assert "hbbft_amd/csrc/kernels.hip" in files and "include/hbrbc.h" in files
+
+
 def test_merkle_proof_is_host_data_movement():
     """MerkleTree::proof only copies sibling digests: checkable without a GPU."""
     for n in [1, 4, 7, 9, 17, 64, 250]:
