@@ -84,6 +84,12 @@ def parse():
                     help="instances per GPU of the cfg2 / cfg5 objects (default: their config)")
     ap.add_argument("--streams", type=int, default=1,
                     help="instance mode: sub-batches per step, each on its own HIP stream")
+    ap.add_argument("--ipipes", type=int, default=1,
+                    help="instance mode (headline): step pipelines, each with its own buffers "
+                         "and HIP stream, step i on pipe i %% ipipes")
+    ap.add_argument("--rider-pipes", type=int, default=2,
+                    help="step pipelines of the cfg2 object (its 65,536-sponge launches fill one "
+                         "wave per SIMD; two pipelines run two side by side)")
     ap.add_argument("--stagger", action="store_true",
                     help="with --streams > 1: each sub-batch starts after the previous one's encode")
     ap.add_argument("--no-leaf-reuse", action="store_true",
@@ -201,7 +207,7 @@ def gen_present(torch, seed, first, count, n, n_erase, dev):
 
 # --------------------------------------------------------------- accounting --
 def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase, elapsed,
-                config, unframe_fused=False):
+                config, unframe_fused=False, pipes=1):
     """Roofline of the dominant kernel from live per-stage HIP-event times.
     Sponge kernels are VALU-bound (Keccak-f[1600]); the HBM view is reported
     beside it."""
@@ -263,10 +269,20 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
          "pipeline_alg_bytes_per_step": step_bytes, "stages": per_stage,
          "pipeline_hbm_frac": step_bytes / (elapsed / steps) / 1e9 / HBM_PEAK_GBS,
          "pipeline_frac_of_measured_copy": step_bytes / (elapsed / steps) / 1e9 / HBM_COPY_GBS}
+    if pipes > 1:
+        # launches of concurrent pipelines overlap: a launch's span includes
+        # the other pipe's kernels, so the per-launch rate above understates
+        # the kernel; `aggregate` is the dominant kernel's work of every timed
+        # launch over the whole wall time (a lower bound of its true rate)
+        r["concurrent_pipes"] = pipes
+        work = (perms[dom] if dom in perms else alg[dom]) * dom_launches
+        r["aggregate"] = {"per_s": work / elapsed, "unit": "perms/s" if dom in perms else "B/s"}
     if dom in perms:
         opp, src = valu_ops_per_perm(config)
         pps = perms[dom] / t
         ops = pps * opp / 1e12
+        if pipes > 1:
+            r["aggregate"]["frac"] = r["aggregate"]["per_s"] * opp / VALU_PEAK_OPS
         r.update({"bound": "valu", "achieved": ops, "peak": VALU_PEAK_OPS / 1e12,
                   "unit": "T lane-ops/s", "frac": ops * 1e12 / VALU_PEAK_OPS,
                   "perms_per_launch": perms[dom], "perms_per_s": pps,
@@ -395,7 +411,7 @@ def cpu_baseline(args, n, f, plen, n_erase, config):
 
 # -------------------------------------------------------------- instance mode --
 def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=None,
-                  streams=None, leaf_reuse=True, encode_merkle=False):
+                  streams=None, leaf_reuse=True, encode_merkle=False, pipes=None):
     """One instance-mode object: `config` labels it (default --config); the
     headline passes streams / leaf_reuse from the command line, the riders
     (cfg2, cfg5) run one stream without the leaf-reuse variant, and cfg2 adds
@@ -430,18 +446,39 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         for sb in subs_rb:   # one fixed pattern: its specialised decoder (rse's cached matrix)
             sb.specialise_decoder(present[0].cpu().numpy())
         pool = [present]
-    slab = torch.empty((count, n, stride), dtype=torch.uint8, device=dev)
-    nodes = torch.empty((count, rb.node_count, 32), dtype=torch.uint8, device=dev)
-    nodes2 = torch.empty_like(nodes)
-    roots = torch.empty((count, 32), dtype=torch.uint8, device=dev)
+    # step pipelines (--ipipes / `pipes`): each with its own buffers, context
+    # and HIP stream, step i on pipe i % npipe -- two whole batches in flight,
+    # so a sponge launch that fills one wave per SIMD (cfg2: 65,536 sponges)
+    # runs beside the other pipe's (every step still does all its work)
+    npipe = max(1, args.ipipes if pipes is None else pipes)
+    assert npipe == 1 or nsub == 1, "step pipelines and sub-batch streams do not combine"
     ds = max(rb.dslots, 1)
-    digests = torch.empty((count, n, ds, 32), dtype=torch.uint8, device=dev)
-    ndig = torch.empty((count, n), dtype=torch.uint8, device=dev)
-    ok = torch.empty((count, n), dtype=torch.uint8, device=dev)
     ostride = (k * S + 15) // 16 * 16
-    out = torch.empty((count, ostride), dtype=torch.uint8, device=dev)
-    plen_out = torch.empty(count, dtype=torch.int32, device=dev)
-    status = torch.empty(count, dtype=torch.int32, device=dev)
+
+    def buffers():
+        nodes_ = torch.empty((count, rb.node_count, 32), dtype=torch.uint8, device=dev)
+        return {"slab": torch.empty((count, n, stride), dtype=torch.uint8, device=dev),
+                "nodes": nodes_, "nodes2": torch.empty_like(nodes_),
+                "roots": torch.empty((count, 32), dtype=torch.uint8, device=dev),
+                "digests": torch.empty((count, n, ds, 32), dtype=torch.uint8, device=dev),
+                "ndig": torch.empty((count, n), dtype=torch.uint8, device=dev),
+                "ok": torch.empty((count, n), dtype=torch.uint8, device=dev),
+                "out": torch.empty((count, ostride), dtype=torch.uint8, device=dev),
+                "plen_out": torch.empty(count, dtype=torch.int32, device=dev),
+                "status": torch.empty(count, dtype=torch.int32, device=dev)}
+    bufs = [buffers() for _ in range(npipe)]
+    B0 = bufs[0]
+    slab, nodes, nodes2, roots = B0["slab"], B0["nodes"], B0["nodes2"], B0["roots"]
+    digests, ndig, ok, out = B0["digests"], B0["ndig"], B0["ok"], B0["out"]
+    plen_out, status = B0["plen_out"], B0["status"]
+    pipe_rb = [rb] + [hb.RbcBatch(n, f, device=local) for _ in range(npipe - 1)]
+    if erase != "f":
+        for sb in pipe_rb[1:]:
+            sb.specialise_decoder(present[0].cpu().numpy())
+    warm = max(args.warmup, npipe)      # every pipe has stepped before the check
+    if erase == "f" and warm > args.warmup:
+        pool += [gen_present(torch, SEED + s, first, count, n, n_erase, dev)
+                 for s in range(len(pool), warm + args.steps)]
 
     # Transport: the receiver never holds the rows its pattern erases.  Every
     # step overwrites them with garbage (the "erase" stage: one row fill,
@@ -456,12 +493,12 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
     bounds = [(i * count) // nsub for i in range(nsub + 1)]
     erase_spans = []
 
-    def erase_rows(i, q):
+    def erase_rows(i, q, sb=None, B=None):
         sl = slice(bounds[q], bounds[q + 1])
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        subs_rb[q].drop_rows(slab[sl], pool[i % len(pool)][sl], 0xA5)   # hbrbc_drop_rows
+        (sb or subs_rb[q]).drop_rows((B or B0)["slab"][sl], pool[i % len(pool)][sl], 0xA5)
         e1.record()
         if timing_erase[0] is not None:
             timing_erase[0].append((e0, e1))
@@ -474,21 +511,31 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         sb = subs_rb[i]
         sb.reserve(hi - lo)
         subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
+    for sb in pipe_rb[1:]:
+        sb.reserve(count)
+    pipe_streams = [main] if npipe == 1 else [torch.cuda.Stream(dev) for _ in range(npipe)]
 
-    def run_sub(sb, sl, pres, i, q, after_encode=None):
-        sb.frame_encode(payloads[sl], plen, slab[sl])   # frame folded into the encoder
+    def run_sub(sb, sl, pres, i, q, after_encode=None, B=None):
+        B = B or B0
+        slab_, nodes_ = B["slab"], B["nodes"]
+        sb.frame_encode(payloads[sl], plen, slab_[sl])   # frame folded into the encoder
         if after_encode is not None:
             after_encode()
-        sb.merkle(slab[sl], S, nodes[sl])
-        sb.proofs(nodes[sl], digests[sl], ndig[sl])
-        sb.validate(slab[sl], S, digests[sl], ndig[sl], nodes[sl], ok[sl])
-        roots[sl].copy_(nodes[sl, -1, :])      # what the Echo/Ready quorum agreed on
-        erase_rows(i, q)
-        sb.decode(slab[sl], S, pres[sl], roots[sl], nodes2[sl], out[sl], plen_out[sl],
-                  status[sl])
+        sb.merkle(slab_[sl], S, nodes_[sl])
+        sb.proofs(nodes_[sl], B["digests"][sl], B["ndig"][sl])
+        sb.validate(slab_[sl], S, B["digests"][sl], B["ndig"][sl], nodes_[sl], B["ok"][sl])
+        B["roots"][sl].copy_(nodes_[sl, -1, :])      # what the Echo/Ready quorum agreed on
+        erase_rows(i, q, sb, B)
+        sb.decode(slab_[sl], S, pres[sl], B["roots"][sl], B["nodes2"][sl], B["out"][sl],
+                  B["plen_out"][sl], B["status"][sl])
 
     def step(i):
         pres = pool[i % len(pool)]
+        if npipe > 1:
+            p_ = i % npipe
+            with torch.cuda.stream(pipe_streams[p_]):
+                run_sub(pipe_rb[p_], slice(None), pres, i, 0, B=bufs[p_])
+            return
         if nsub == 1:
             run_sub(subs[0][0], subs[0][2], pres, i, 0)
             return
@@ -509,73 +556,85 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         for _, st, _ in subs:
             main.wait_stream(st)
 
-    def check(what):
+    def check(what, pipes_run):
         """Every proof valid, every decode Ok, every payload byte, and the
         decode trees equal to the proposer's -- the rebuilt rows hash to the
         same leaves, so every rebuilt byte is right."""
-        assert bool((ok == 1).all()), "%s: a valid proof was rejected" % what
-        assert bool((status == 0).all()), "%s: decode failed" % what
-        assert bool((plen_out == plen).all()), what
-        assert torch.equal(out[:, :plen], payloads[:, :plen]), "%s: decoded payload differs" % what
-        assert torch.equal(nodes2, nodes), "%s: rebuilt rows differ" % what
+        for p_ in pipes_run:
+            B = bufs[p_]
+            assert bool((B["ok"] == 1).all()), "%s: a valid proof was rejected" % what
+            assert bool((B["status"] == 0).all()), "%s: decode failed" % what
+            assert bool((B["plen_out"] == plen).all()), what
+            assert torch.equal(B["out"][:, :plen], payloads[:, :plen]), \
+                "%s: decoded payload differs" % what
+            assert torch.equal(B["nodes2"], B["nodes"]), "%s: rebuilt rows differ" % what
 
-    for i in range(args.warmup):
+    def begin():   # side streams start after everything queued on the main one
+        for st in pipe_streams[1:] if npipe > 1 else []:
+            st.wait_stream(main)
+    begin()
+    for i in range(warm):
         step(i)
     torch.cuda.synchronize(dev)
     if not args.no_verify:
-        check("warm-up")
+        check("warm-up", range(npipe))
         # the last warm-up step's erased rows were garbage before its decode:
         # poison the payload buffer too, so the timed steps' outputs are theirs
-        out.fill_(0x5A)
-        nodes2.fill_(0x5A)
+        for B in bufs:
+            B["out"].fill_(0x5A)
+            B["nodes2"].fill_(0x5A)
 
-    for sb in subs_rb:
+    all_rb = list(subs_rb) + pipe_rb[1:]
+    for sb in all_rb:
         sb.profile(True)
         sb.profile_reset()
     timing_erase[0] = erase_spans
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    begin()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(warm + i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timing_erase[0] = None
-    for sb in subs_rb:
+    for sb in all_rb:
         sb.profile(False)
     erase_s = sum(a.elapsed_time(b) for a, b in erase_spans) / 1e3
     # one stream: the erase spans are serial with the reference work and come
-    # out of the wall time; sub-batches on several streams overlap them, so
-    # nothing is subtracted there
-    work = elapsed - (erase_s if nsub == 1 else 0.0)
+    # out of the wall time; sub-batches or pipelines on several streams
+    # overlap them, so nothing is subtracted there
+    serial = nsub == 1 and npipe == 1
+    work = elapsed - (erase_s if serial else 0.0)
     elapsed_all = max_over_ranks(elapsed, world, dev)
     elapsed = max_over_ranks(work, world, dev)
     verified = False
     if not args.no_verify:
-        check("last timed step")   # the outputs of the last timed step, from garbage rows
+        # the outputs of each pipe's last timed step, from garbage rows
+        check("last timed step", sorted({(warm + j) % npipe for j in range(args.steps)}))
         verified = True
     stages = {}
-    for sb in subs_rb:
+    for sb in all_rb:
         for st_name, (ms, cnt) in sb.profile_read().items():
             a0, c0 = stages.get(st_name, (0.0, 0))
             stages[st_name] = (a0 + ms, c0 + cnt)
     stages["erase"] = (erase_s * 1e3, len(erase_spans))
     value = float(count) * plen * world * args.steps / elapsed / 1e9
     lr = None
-    if leaf_reuse and not args.no_leaf_reuse and nsub == 1 and erase == "f":
+    if leaf_reuse and not args.no_leaf_reuse and nsub == 1 and npipe == 1 and erase == "f":
         lr = run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, digests,
                             ndig, ok, out, plen_out, status, S, n, f, world, dev,
                             erase_rows, timing_erase)
     em = None
     if encode_merkle:
-        em = run_encode_merkle(args, rb, payloads, plen, slab, nodes, digests, ndig, S, world,
+        em = run_encode_merkle(args, pipe_rb, payloads, plen, bufs, pipe_streams, S, world,
                                dev, count)
     roof = roofline_of(stages, args.steps, count / nsub, n, k, m, S, plen, rb.node_count,
                        rb.dslots, n_erase, elapsed, config,
-                       unframe_fused=rb.unframe_fused(S, out.stride(0)))
+                       unframe_fused=rb.unframe_fused(S, out.stride(0)), pipes=npipe)
     roof["unframe_fused"] = rb.unframe_fused(S, out.stride(0))
     r = {
         "value": value, "unit": "GB/s", "ms_per_step": elapsed / args.steps * 1e3,
@@ -588,7 +647,8 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
                                                 "f random" if erase == "f" else "worst-case"),
                    "n": n, "f": f, "payload_bytes": plen, "shard_len": S,
                    "instances_per_gpu": count, "global_batch": count * world,
-                   "parallelism": "instance-sharded x%d" % world, "streams_per_gpu": nsub},
+                   "parallelism": "instance-sharded x%d" % world, "streams_per_gpu": nsub,
+                   "step_pipelines": npipe},
         "n_erase": n_erase, "f": f, "leaf_reuse": lr,
         "verified_last_timed_step": verified,
         "decode_input": ("every step overwrites the %d erased rows of each instance with garbage "
@@ -685,45 +745,71 @@ def run_leaf_reuse(args, rb, payloads, plen, pool, slab, nodes, nodes2, roots, d
                     "and their leaves are garbage before every decode)"}
 
 
-def run_encode_merkle(args, rb, payloads, plen, slab, nodes, digests, ndig, S, world, dev, count):
+def run_encode_merkle(args, rbs, payloads, plen, bufs, streams, S, world, dev, count):
     """BASELINE cfg2's own metric: encode + Merkle only -- the proposer half
     of send_shards (broadcast.rs:170-225: frame, Coding::encode,
     MerkleTree::from_vec, one proof per shard) over the same batch, timed
-    like the headline; the tree and proofs are checked against the full
+    like the headline (step i on pipeline i % len(rbs), each with its own
+    buffers and stream); the trees and proofs are checked against the full
     step's (which validated every proof)."""
     import torch
-    ref = nodes.clone()
+    npipe = len(rbs)
+    refs = [B["nodes"].clone() for B in bufs]
+    main = torch.cuda.current_stream(dev)
 
-    def step():
-        rb.frame_encode(payloads, plen, slab)
-        rb.merkle(slab, S, nodes)
-        rb.proofs(nodes, digests, ndig)
-    for _ in range(max(1, args.warmup)):
-        step()
+    def step(i):
+        p_ = i % npipe
+        B, rb = bufs[p_], rbs[p_]
+        with torch.cuda.stream(streams[p_]):
+            rb.frame_encode(payloads, plen, B["slab"])
+            rb.merkle(B["slab"], S, B["nodes"])
+            rb.proofs(B["nodes"], B["digests"], B["ndig"])
+
+    def begin():
+        for st in streams:
+            if st != main:
+                st.wait_stream(main)
+
+    def check(what):
+        for B, ref in zip(bufs, refs):
+            assert torch.equal(B["nodes"], ref), "encode+Merkle %s: trees differ" % what
+    warm = max(1, args.warmup, npipe)
+    for B in bufs:
+        B["nodes"].fill_(0x5A)
+    begin()
+    for i in range(warm):
+        step(i)
     torch.cuda.synchronize(dev)
     if not args.no_verify:
-        assert torch.equal(nodes, ref), "encode+Merkle: trees differ"
-    rb.profile(True)
-    rb.profile_reset()
+        check("warm-up")
+    for rb in rbs:
+        rb.profile(True)
+        rb.profile_reset()
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize(dev)
+    begin()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(warm + i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
-    rb.profile(False)
-    stages = {k_: v_[0] / args.steps for k_, v_ in rb.profile_read().items() if v_[1]}
+    stages = {}
+    for rb in rbs:
+        rb.profile(False)
+        for k_, v_ in rb.profile_read().items():
+            if v_[1]:
+                stages[k_] = stages.get(k_, 0.0) + v_[0] / args.steps
     if not args.no_verify:
-        assert torch.equal(nodes, ref), "encode+Merkle: trees differ after the timed steps"
-    del ref
+        check("after the timed steps")
+    del refs
     return {"metric": "RBC encode+Merkle payload GB/s (frame, encode, tree, N proofs)",
             "value": float(count) * plen * world * args.steps / elapsed / 1e9, "unit": "GB/s",
-            "ms_per_step": elapsed / args.steps * 1e3, "stages_ms_per_step": stages}
+            "ms_per_step": elapsed / args.steps * 1e3, "stages_ms_per_step": stages,
+            "step_pipelines": npipe}
 
 
 def max_over_ranks(x, world, dev):
@@ -1212,7 +1298,9 @@ def compact_line(full, detail_path=None):
             line[k] = full[k]
     objs = [("leaf_reuse", ()),
             ("cfg2", (("encode_merkle", ("encode_merkle", "value")),
-                      ("encode_merkle_ms", ("encode_merkle", "ms_per_step")))),
+                      ("encode_merkle_ms", ("encode_merkle", "ms_per_step")),
+                      ("pipes", ("config", "step_pipelines")),
+                      ("roofline_aggregate_frac", ("roofline", "aggregate", "frac")))),
             ("cfg5", ()),
             ("threshold_decrypt", (("cpu_baseline", ("cpu_baseline", "value")),
                                    ("cpu_cores", ("cpu_baseline", "cores")))),
@@ -1414,7 +1502,8 @@ def real_phases(args, world, rank, dev, local):
             ph.append((cfg, fresh(lambda n_=n_, plen_=plen_, cnt_=cnt_, er_=er_, cfg=cfg:
                                   run_instances(args, n_, plen_, args.rider_count or cnt_, er_,
                                                 rank, world, dev, local, config=cfg, streams=1,
-                                                leaf_reuse=False, encode_merkle=cfg == "cfg2"))))
+                                                leaf_reuse=False, encode_merkle=cfg == "cfg2",
+                                                pipes=args.rider_pipes if cfg == "cfg2" else 1))))
     if args.f4_checks > 0:
         ph.append(("threshold_decrypt", fresh(lambda: run_threshold(args, rank, world, dev))))
     if args.mode in ("validators", "both"):

@@ -616,14 +616,19 @@ struct Sm {
             }
         } else if (!overflow) {
             rotate_tail(m0, m1, f0, f1);
-            // flag the Echo that the step's EchoHash now directly follows
-            // (Echo to all but the right nodes, EchoHash to the right ones)
-            for (uint32_t q = m0; q + 1 < nout; ++q) {
-                uint32_t &hq = out[(size_t)q * rec];
-                if ((hq & kKindMask) == K_ECHO && (out[(size_t)(q + 1) * rec] & kKindMask) == K_ECHO_HASH) {
-                    hq |= kPairFlag;
-                    break;
-                }
+            // After the rotation send_echo_left's records are [m0, m0 + ne),
+            // the EchoHash step's follow.  Flag only send_echo_left's own Echo
+            // (at m0, to all but the right nodes), and only when the step's
+            // EchoHash (to the right nodes) directly follows it -- its Echo
+            // step emitted one record.  Any other Echo (send_echo_remaining's,
+            // to the right nodes too) is never flagged: its targets overlap
+            // the EchoHash's, and the receiver's merged step assumes disjoint
+            // targets.
+            const uint32_t ne = nout - m1;
+            if (ne == 1 && m0 + 1 < nout) {
+                uint32_t &h = out[(size_t)m0 * rec];
+                if ((h & kKindMask) == K_ECHO && (out[(size_t)(m0 + 1) * rec] & kKindMask) == K_ECHO_HASH)
+                    h |= kPairFlag;
             }
         }
     }
