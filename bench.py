@@ -1296,6 +1296,8 @@ def compact_line(full, detail_path=None):
     for k in ("value_incl_erase", "stages_ms_per_step"):
         if k in full:
             line[k] = full[k]
+    if "encode_merkle" in full:   # --config cfg2: BASELINE's encode+Merkle rate
+        line["encode_merkle"] = _get(full, "encode_merkle", "value")
     objs = [("leaf_reuse", ()),
             ("cfg2", (("encode_merkle", ("encode_merkle", "value")),
                       ("encode_merkle_ms", ("encode_merkle", "ms_per_step")),
@@ -1336,7 +1338,7 @@ def assemble(args, world, res, cpu):
             "config": head["config"], "roofline": head["roofline"], "cpu_baseline": cpu,
             "stages_ms_per_step": head["stages_ms_per_step"],
         }
-        for k in ("value_incl_erase", "ms_per_step_incl_erase", "decode_input"):
+        for k in ("value_incl_erase", "ms_per_step_incl_erase", "decode_input", "encode_merkle"):
             if k in head:
                 line[k] = head[k]
         if head.get("leaf_reuse") is not None:

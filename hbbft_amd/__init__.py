@@ -533,9 +533,14 @@ class RbcBatch:
         self.dslots = max_proof_len(n)
 
     # -- layout helpers -----------------------------------------------------
+    # row slot alignment of the slabs (bytes; A/B knob HBRBC_ROW_ALIGN, a
+    # multiple of 16): rows are S bytes rounded up to it
+    ROW_ALIGN = int(os.environ.get("HBRBC_ROW_ALIGN", "16"))
+
     @staticmethod
     def stride_for(S):
-        return (S + 15) // 16 * 16
+        a = RbcBatch.ROW_ALIGN
+        return (S + a - 1) // a * a
 
     def alloc_slab(self, count, S):
         import torch
