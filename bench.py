@@ -513,7 +513,11 @@ def run_instances(args, n, plen, count, erase, rank, world, dev, local, config=N
         subs.append((sb, torch.cuda.Stream(dev) if nsub > 1 else main, slice(lo, hi)))
     for sb in pipe_rb[1:]:
         sb.reserve(count)
-    pipe_streams = [main] if npipe == 1 else [torch.cuda.Stream(dev) for _ in range(npipe)]
+    # each pipeline on its context's own stream: the contexts' streams are
+    # created one after the other, so they sit on successive hardware queues
+    # (two torch pool streams can share one queue, and then never overlap:
+    # DESIGN.md section 4, rejected list)
+    pipe_streams = [main] if npipe == 1 else [sb.own_stream() for sb in pipe_rb]
 
     def run_sub(sb, sl, pres, i, q, after_encode=None, B=None):
         B = B or B0
