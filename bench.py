@@ -869,7 +869,12 @@ def run_validators(args, n, plen, count, rank, world, dev, local, config=None):
     npipe = max(1, args.vpipes) if overlap else 1
     pipe_sbs = [sb] + [ShardedBroadcast(n, count, plen, rank, world, device=local, sm_slots=2)
                        for _ in range(npipe - 1)]
-    pipe_streams = [(torch.cuda.Stream(dev), torch.cuda.Stream(dev)) for _ in range(npipe)]
+    if os.environ.get("HBRBC_BENCH_OWNQ", "0") == "1":
+        # A/B: each pipeline's data plane on its context's own stream (the
+        # contexts' streams sit on successive hardware queues)
+        pipe_streams = [(p_.rb.own_stream(), torch.cuda.Stream(dev)) for p_ in pipe_sbs]
+    else:
+        pipe_streams = [(torch.cuda.Stream(dev), torch.cuda.Stream(dev)) for _ in range(npipe)]
 
     def step():
         if world > 1:   # sub-batches with every exchange in flight behind compute

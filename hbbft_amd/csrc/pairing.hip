@@ -417,7 +417,7 @@ DEV void fp6_mul_v(Fp6 &r, const Fp6 &a) {
     r.c0 = t;
 }
 
-NOINL void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
+DEV void fp6_mul_in(Fp6 &r, const Fp6 &a, const Fp6 &b) {
     Fp2 aa, bb, cc, s, t, t1, t2, t3;
     fp2_mul_in(aa, a.c0, b.c0);
     fp2_mul_in(bb, a.c1, b.c1);
@@ -446,6 +446,7 @@ NOINL void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) {
     r.c1 = t2;
     r.c2 = t3;
 }
+NOINL void fp6_mul(Fp6 &r, const Fp6 &a, const Fp6 &b) { fp6_mul_in(r, a, b); }
 
 // (a0 + a1 v + a2 v^2)(c0 + c1 v)
 DEV void fp6_mul_by_01(Fp6 &r, const Fp6 &a, const Fp2 &c0, const Fp2 &c1) {
@@ -538,34 +539,43 @@ DEV bool fp12_is_one(const Fp12 &a) {
 
 DEV void fp12_conj(Fp12 &r, const Fp12 &a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
 
+// HB_FE_INL: the Fp6 products of the full Fp12 product inlined into it (A/B)
+#ifndef HB_FE_INL
+#define HB_FE_INL 0
+#endif
 NOINL void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) {
     Fp6 aa, bb, s, t;
-    fp6_mul(aa, a.c0, b.c0);
-    fp6_mul(bb, a.c1, b.c1);
+    if (HB_FE_INL) fp6_mul_in(aa, a.c0, b.c0); else fp6_mul(aa, a.c0, b.c0);
+    if (HB_FE_INL) fp6_mul_in(bb, a.c1, b.c1); else fp6_mul(bb, a.c1, b.c1);
     fp6_add(s, a.c0, a.c1);
     fp6_add(t, b.c0, b.c1);
-    fp6_mul(s, s, t);
+    if (HB_FE_INL) fp6_mul_in(s, s, t); else fp6_mul(s, s, t);
     fp6_sub(s, s, aa);
     fp6_sub(r.c1, s, bb);
     fp6_mul_v(bb, bb);
     fp6_add(r.c0, aa, bb);
 }
 
-NOINL void fp12_sqr(Fp12 &r, const Fp12 &a) {
+// INL: the Fp6 products inlined (no call boundary inside the unit, so no
+// stack traffic for their operands; tools/fp_microbench.hip: the same 26.8 k
+// lane-ops per squaring run 1.47x faster in this form)
+template <bool INL>
+DEV void fp12_sqr_t(Fp12 &r, const Fp12 &a) {
     Fp6 ab, s, t;
-    fp6_mul(ab, a.c0, a.c1);
+    if (INL) fp6_mul_in(ab, a.c0, a.c1); else fp6_mul(ab, a.c0, a.c1);
     fp6_add(s, a.c0, a.c1);
     fp6_mul_v(t, a.c1);
     fp6_add(t, t, a.c0);
-    fp6_mul(s, s, t);
+    if (INL) fp6_mul_in(s, s, t); else fp6_mul(s, s, t);
     fp6_sub(s, s, ab);
     fp6_mul_v(t, ab);
     fp6_sub(r.c0, s, t);
     fp6_dbl(r.c1, ab);
 }
+NOINL void fp12_sqr(Fp12 &r, const Fp12 &a) { fp12_sqr_t<false>(r, a); }
 
 // f * (c0 + c1 v + c4 v w): the sparse line value
-NOINL void fp12_mul_by_014(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4) {
+DEV void fp12_mul_by_014_in(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4) {
     Fp6 aa, bb, s;
     Fp2 o;
     fp6_mul_by_01(aa, f.c0, c0, c1);
@@ -577,6 +587,9 @@ NOINL void fp12_mul_by_014(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4)
     fp6_sub(f.c1, s, bb);
     fp6_mul_v(bb, bb);
     fp6_add(f.c0, bb, aa);
+}
+NOINL void fp12_mul_by_014(Fp12 &f, const Fp2 &c0, const Fp2 &c1, const Fp2 &c4) {
+    fp12_mul_by_014_in(f, c0, c1, c4);
 }
 
 DEV void fp12_inv(Fp12 &r, const Fp12 &a) {
@@ -1153,11 +1166,33 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_P
     }
 }
 
+// The prepared Miller loop's per-bit work as units of their own (A/B knob
+// HB_MILLER_INL): 0 = out-of-line squaring and line application (their
+// Fp6 operands through the stack); 1 = the squaring's Fp6 products inlined
+// into it; 2 = also the sparse product inlined into the line application.
+#ifndef HB_MILLER_INL
+#define HB_MILLER_INL 2   // round 6: Miller 85.97 -> 80.0-80.5 ms per 262,144 checks (r6e)
+#endif
+#if HB_MILLER_INL < 2
 NOINL void apply_prepared(Fp12 &f, const uint32_t *line, const Fp &xp, const Fp &yp) {
     Fp2 l0, l1, l4;
     load_line(line, l0, l1, l4);
     apply_line(f, l0, l1, l4, xp, yp);
 }
+#endif
+NOINL void miller_sqr(Fp12 &f) { fp12_sqr_t<(HB_MILLER_INL >= 1)>(f, f); }
+NOINL void apply_prepared_in(Fp12 &f, const uint32_t *line, const Fp &xp, const Fp &yp) {
+    Fp2 l0, l1, l4, a, b;
+    load_line(line, l0, l1, l4);
+    fp2_mul_fp(a, l1, xp);
+    fp2_mul_fp(b, l4, yp);
+    fp12_mul_by_014_in(f, l0, a, b);
+}
+#if HB_MILLER_INL >= 2
+#define HB_APPLY_PREPARED apply_prepared_in
+#else
+#define HB_APPLY_PREPARED apply_prepared
+#endif
 
 // One lane per check e(a, b) == e(c, d) with b, d prepared (points ib[i],
 // id[i] of the table): g1 holds a, c at rows 2i, 2i+1.  Lanes of a wave
@@ -1188,14 +1223,14 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_P
         const uint32_t *p1 = prep + (size_t)qb * kLines * kLineWords;
         const uint32_t *p2 = prep + (size_t)qd * kLines * kLineWords;
         for (int b = 62; b >= 0; --b) {
-            fp12_sqr(f, f);
-            if (on1) apply_prepared(f, p1, xa, ya);
-            if (on2) apply_prepared(f, p2, xc, yc);
+            if (HB_MILLER_INL) miller_sqr(f); else fp12_sqr(f, f);
+            if (on1) HB_APPLY_PREPARED(f, p1, xa, ya);
+            if (on2) HB_APPLY_PREPARED(f, p2, xc, yc);
             p1 += kLineWords;
             p2 += kLineWords;
             if ((kXAbs >> b) & 1u) {
-                if (on1) apply_prepared(f, p1, xa, ya);
-                if (on2) apply_prepared(f, p2, xc, yc);
+                if (on1) HB_APPLY_PREPARED(f, p1, xa, ya);
+                if (on2) HB_APPLY_PREPARED(f, p2, xc, yc);
                 p1 += kLineWords;
                 p2 += kLineWords;
             }
@@ -1255,7 +1290,10 @@ DEV void store_be48(uint8_t *dst, const Fp &a) {
 // (1: a pairing, 2: a check) are multiplied first.  gt_out (if set) gets the
 // 576-byte GT value; ok_out (if set) gets 1 if the value is 1 (the check
 // holds), 0 if not, 2 if an input point was invalid.
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void final_exp_kernel(
+#ifndef HB_FE_WPE
+#define HB_FE_WPE HB_PAIR_WPE   // A/B: the final exponentiation's own occupancy
+#endif
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_FE_WPE, HB_FE_WPE))) void final_exp_kernel(
     const uint32_t *__restrict__ ws, size_t n_miller, size_t n_out, int per_out,
     const uint8_t *__restrict__ status, uint8_t *__restrict__ gt_out,
     uint8_t *__restrict__ ok_out) {
