@@ -127,6 +127,40 @@ __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
     out[g] = fold12(f);
 }
 
+// the final exponentiation's pieces: f^|x| (fp12_exp_by_x: 62 cyclotomic
+// squarings + 5 products) and the whole final exponentiation
+__global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_expx(
+    int iters, uint32_t *out) {
+    const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
+    Fp12 f;
+    seed12(f, g);
+    for (int it = 0; it < iters; ++it) fp12_exp_by_x(f, f, 0);
+    out[g] = fold12(f);
+}
+
+__global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fe(
+    int iters, uint32_t *out) {
+    const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
+    Fp12 f;
+    seed12(f, g);
+    for (int it = 0; it < iters; ++it) {
+        Fp12 r;
+        final_exp(r, f);
+        f = r;
+    }
+    out[g] = fold12(f);
+}
+
+__global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fp12mul(
+    int iters, uint32_t *out) {
+    const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
+    Fp12 f, h;
+    seed12(f, g);
+    seed12(h, g + 5);
+    for (int it = 0; it < iters; ++it) fp12_mul(f, f, h);
+    out[g] = fold12(f);
+}
+
 }  // namespace
 }  // namespace hbrbc
 
@@ -153,7 +187,10 @@ int main(int argc, char **argv) {
     } ks[] = {{"fp2mul", mb_fp2mul, 2000, 1},
               {"fp12sqr", mb_fp12sqr, 200, 12},      // 2 Fp6 products x 6 Fp2 products
               {"fp12sqr_inl", mb_fp12sqr_inl, 200, 12},
-              {"cyclo", mb_cyclo, 200, 9}};           // 3 fp4_sqr x 3 Fp2 squarings
+              {"cyclo", mb_cyclo, 200, 9},            // 3 fp4_sqr x 3 Fp2 squarings
+              {"fp12mul", mb_fp12mul, 100, 18},       // 3 Fp6 products x 6 Fp2 products
+              {"expx", mb_expx, 4, 62 * 9 + 5 * 18},
+              {"fe", mb_fe, 1, 0}};
     for (auto &k : ks) {
         hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(kMbBlock), 0, 0, 4, out);   // warm-up
         CK(hipDeviceSynchronize());
