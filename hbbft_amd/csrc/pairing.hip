@@ -543,18 +543,20 @@ DEV void fp12_conj(Fp12 &r, const Fp12 &a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
 #ifndef HB_FE_INL
 #define HB_FE_INL 0
 #endif
-NOINL void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) {
+template <bool INL>
+DEV void fp12_mul_t(Fp12 &r, const Fp12 &a, const Fp12 &b) {
     Fp6 aa, bb, s, t;
-    if (HB_FE_INL) fp6_mul_in(aa, a.c0, b.c0); else fp6_mul(aa, a.c0, b.c0);
-    if (HB_FE_INL) fp6_mul_in(bb, a.c1, b.c1); else fp6_mul(bb, a.c1, b.c1);
+    if (INL) fp6_mul_in(aa, a.c0, b.c0); else fp6_mul(aa, a.c0, b.c0);
+    if (INL) fp6_mul_in(bb, a.c1, b.c1); else fp6_mul(bb, a.c1, b.c1);
     fp6_add(s, a.c0, a.c1);
     fp6_add(t, b.c0, b.c1);
-    if (HB_FE_INL) fp6_mul_in(s, s, t); else fp6_mul(s, s, t);
+    if (INL) fp6_mul_in(s, s, t); else fp6_mul(s, s, t);
     fp6_sub(s, s, aa);
     fp6_sub(r.c1, s, bb);
     fp6_mul_v(bb, bb);
     fp6_add(r.c0, aa, bb);
 }
+NOINL void fp12_mul(Fp12 &r, const Fp12 &a, const Fp12 &b) { fp12_mul_t<HB_FE_INL != 0>(r, a, b); }
 
 // INL: the Fp6 products inlined (no call boundary inside the unit, so no
 // stack traffic for their operands; tools/fp_microbench.hip: the same 26.8 k
@@ -673,12 +675,19 @@ void fp12_cyclo_sqr(Fp12 &f) {
 
 // f^x for the BLS parameter x < 0 (the crate's exp_by_x: pow by |x|, then
 // conjugate -- the inverse on the cyclotomic subgroup).  `shift` gives |x|>>1.
+// HB_EXPX_INL (A/B): 1 = the five products by `a` inlined too (Fp6 products
+// inlined), so the whole f^|x| is one unit with no call inside its loop
+#ifndef HB_EXPX_INL
+#define HB_EXPX_INL 0
+#endif
 NOINL void fp12_exp_by_x(Fp12 &r, const Fp12 &a, int shift) {
     const uint64_t e = kXAbs >> shift;
     Fp12 acc = a;
     for (int b = 62 - shift; b >= 0; --b) {
         fp12_cyclo_sqr(acc);
-        if ((e >> b) & 1u) fp12_mul(acc, acc, a);
+        if ((e >> b) & 1u) {
+            if (HB_EXPX_INL) fp12_mul_t<true>(acc, acc, a); else fp12_mul(acc, acc, a);
+        }
     }
     fp12_conj(r, acc);
 }
