@@ -53,9 +53,11 @@ CONFIGS = {
     # on one GPU, profiles/r4aa_vcount_ab.txt; G=8 footprint 0.3 of HBM, tests/test_sharded.py)
     "cfg3": (64, 256 << 10, 32768, "f", 8192),
     "cfg4": (128, 256 << 10, 16384, "f", 4096),
-    # cfg2 keeps BASELINE's batch of 4096; cfg4 / cfg5 name none: 16384 / 2048
-    # instances (+1 / +5 % over 8192 / 1024, profiles/r4ac_count_ab.txt)
-    "cfg5": (250, 4 << 20, 2048, "worst", 128),
+    # cfg2 keeps BASELINE's batch of 4096; cfg4 / cfg5 name none: 16384 / 4096
+    # instances (cfg4 +1 % over 8192, profiles/r4ac_count_ab.txt; cfg5 4096:
+    # 86.8 vs 84.1-84.6 GB/s at 2048, profiles/r6k_cfg5_batch_pipes_ab.txt --
+    # four residency rounds of the sponge launches instead of two; ~90 GB)
+    "cfg5": (250, 4 << 20, 4096, "worst", 128),
 }
 METRIC = "RBC encode+Merkle+decode payload GB/s, N=64, 1/8 GPUs; fraction of HBM peak"
 
@@ -231,6 +233,11 @@ def roofline_of(stages, steps, per_launch, n, k, m, S, plen, nc, dslots, n_erase
              "tree_levels": per_launch * (n - 1)}
     live = {s: v for s, v in stages.items() if v[1] > 0}
     dom = max(live, key=lambda s: live[s][0])
+    if pipes > 1 and any(s_ in perms for s_ in live):
+        # concurrent pipelines stretch every launch's span by the other
+        # pipeline's kernels, so spans no longer rank the stages: the sponge
+        # launches carry the step's work (the one-pipeline profile's ranking)
+        dom = max((s_ for s_ in live if s_ in perms), key=lambda s_: live[s_][0])
     dom_ms, dom_launches = live[dom]
     t = dom_ms / 1e3 / max(dom_launches, 1)
     hbm_gbs = alg[dom] / t / 1e9
