@@ -46,7 +46,7 @@ DEV uint32_t fold12(const Fp12 &f) {
 }
 
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fp2mul(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp2 a, b;
     seed_fp(a.c0, g);
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fp12sqr(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp12 f;
     seed12(f, g);
@@ -99,7 +99,7 @@ DEV void fp6_mul_inl(Fp6 &r, const Fp6 &a, const Fp6 &b) {
 }
 
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fp12sqr_inl(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp12 f;
     seed12(f, g);
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_cyclo(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp12 f;
     seed12(f, g);
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
 // the final exponentiation's pieces: f^|x| (fp12_exp_by_x: 62 cyclotomic
 // squarings + 5 products) and the whole final exponentiation
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_expx(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp12 f;
     seed12(f, g);
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fe(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp12 f;
     seed12(f, g);
@@ -152,12 +152,45 @@ __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 __global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_fp12mul(
-    int iters, uint32_t *out) {
+    int iters, uint32_t *out, const uint32_t *) {
     const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
     Fp12 f, h;
     seed12(f, g);
     seed12(h, g + 5);
     for (int it = 0; it < iters; ++it) fp12_mul(f, f, h);
+    out[g] = fold12(f);
+}
+
+// the prepared Miller loop's pieces: one line application (load 72 words,
+// scale two coefficients by P, sparse product) and one whole bit step
+// (squaring + two line applications, as miller_prepared_kernel runs them)
+__global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_apply(
+    int iters, uint32_t *out, const uint32_t *line) {
+    const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
+    Fp12 f;
+    Fp xp, yp;
+    seed12(f, g);
+    seed_fp(xp, g + 3);
+    seed_fp(yp, g + 9);
+    for (int it = 0; it < iters; ++it) apply_prepared_in(f, line + (it & 63) * kLineWords, xp, yp);
+    out[g] = fold12(f);
+}
+
+__global__ __launch_bounds__(kMbBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mb_millerstep(
+    int iters, uint32_t *out, const uint32_t *line) {
+    const uint32_t g = blockIdx.x * kMbBlock + threadIdx.x;
+    Fp12 f;
+    Fp xa, ya, xc, yc;
+    seed12(f, g);
+    seed_fp(xa, g + 3);
+    seed_fp(ya, g + 9);
+    seed_fp(xc, g + 5);
+    seed_fp(yc, g + 11);
+    for (int it = 0; it < iters; ++it) {
+        miller_sqr(f);
+        HB_APPLY_PREPARED(f, line + (it & 63) * kLineWords, xa, ya);
+        HB_APPLY_PREPARED(f, line + ((it + 7) & 63) * kLineWords, xc, yc);
+    }
     out[g] = fold12(f);
 }
 
@@ -177,11 +210,17 @@ int main(int argc, char **argv) {
     using namespace hbrbc;
     const int lanes = argc > 1 ? atoi(argv[1]) : 256 * 4 * 2 * 64;   // 2 waves per SIMD
     const int blocks = lanes / kMbBlock;
-    uint32_t *out;
+    uint32_t *out, *line;
     CK(hipMalloc(&out, (size_t)lanes * 4));
+    {   // 64 line records of arbitrary words (timing only)
+        std::vector<uint32_t> h(64 * kLineWords);
+        for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)(i * 2654435761u) & 0x0FFFFFFFu;
+        CK(hipMalloc(&line, h.size() * 4));
+        CK(hipMemcpy(line, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    }
     struct K {
         const char *name;
-        void (*fn)(int, uint32_t *);
+        void (*fn)(int, uint32_t *, const uint32_t *);
         int iters;
         int fp2_products;   // Fp2 products (or squarings) per iteration
     } ks[] = {{"fp2mul", mb_fp2mul, 2000, 1},
@@ -190,15 +229,17 @@ int main(int argc, char **argv) {
               {"cyclo", mb_cyclo, 200, 9},            // 3 fp4_sqr x 3 Fp2 squarings
               {"fp12mul", mb_fp12mul, 100, 18},       // 3 Fp6 products x 6 Fp2 products
               {"expx", mb_expx, 4, 62 * 9 + 5 * 18},
-              {"fe", mb_fe, 1, 0}};
+              {"fe", mb_fe, 1, 0},
+              {"apply", mb_apply, 100, 13},          // 13 Fp2 products (+ 2 Fp2 x Fp)
+              {"millerstep", mb_millerstep, 50, 12 + 2 * 13}};
     for (auto &k : ks) {
-        hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(kMbBlock), 0, 0, 4, out);   // warm-up
+        hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(kMbBlock), 0, 0, 4, out, line);   // warm-up
         CK(hipDeviceSynchronize());
         hipEvent_t a, b;
         CK(hipEventCreate(&a));
         CK(hipEventCreate(&b));
         CK(hipEventRecord(a, 0));
-        hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(kMbBlock), 0, 0, k.iters, out);
+        hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(kMbBlock), 0, 0, k.iters, out, line);
         CK(hipEventRecord(b, 0));
         CK(hipEventSynchronize(b));
         float ms = 0.f;
@@ -209,5 +250,6 @@ int main(int argc, char **argv) {
                k.name, lanes, k.iters, ms, units / (ms * 1e-3), units * k.fp2_products / (ms * 1e-3));
     }
     CK(hipFree(out));
+    CK(hipFree(line));
     return 0;
 }
