@@ -195,3 +195,30 @@ def test_phases_stuck_collective_prints_the_line():
     assert line["value"] > 0 and line["cfg2"]["value"] > 0
     assert "timeout" in line["validators"]["error"]
     assert "validators_cfg4" not in line
+
+
+def test_roofline_with_step_pipelines():
+    """With two step pipelines the launch spans overlap: the encode's span can
+    exceed the sponges', yet the dominant kernel stays a sponge stage and the
+    line's `frac` is the aggregate rate (every sponge launch's permutations
+    over the wall time), the per-launch figure kept beside it."""
+    n, k, m, plen, count, steps = 16, 6, 10, 1 << 20, 4096, 10
+    S = (plen + 4 + k - 1) // k
+    L = (S + 1 + 135) // 136
+    nc, dsl = 31, 4
+    # stage: (ms summed over the timed steps, launches)
+    stages = {"encode": (600.0, 2 * steps), "leaf_hash": (550.0, 2 * steps),
+              "validate": (300.0, steps), "tree_levels": (3.0, 2 * steps),
+              "proofs": (1.0, steps), "reconstruct": (50.0, steps), "frame": (0.0, 0)}
+    elapsed = 0.33
+    r = bench.roofline_of(stages, steps, count, n, k, m, S, plen, nc, dsl, 5, elapsed, "cfgX",
+                          pipes=2)
+    assert r["kernel"] == "leaf_hash" and r["bound"] == "valu" and r["concurrent_pipes"] == 2
+    perms = (count * n * L * 2 * steps + count * (n * L + n * dsl) * steps
+             + count * (n - 1) * 2 * steps)
+    opp, _ = bench.valu_ops_per_perm("cfgX")
+    assert abs(r["aggregate"]["perms_per_s"] - perms / elapsed) < 1e-6 * perms / elapsed
+    assert abs(r["frac"] - perms / elapsed * opp / bench.VALU_PEAK_OPS) < 1e-9
+    assert r["per_launch_frac"] < r["frac"] and r["profiled"] is None
+    one = bench.roofline_of(stages, steps, count, n, k, m, S, plen, nc, dsl, 5, elapsed, "cfgX")
+    assert one["kernel"] == "encode" and "aggregate" not in one   # one pipeline: spans rank
