@@ -16,7 +16,8 @@ fn main() {
             let root = manifest.parent().expect("hbbft-hip sits beside hbbft_amd/").to_path_buf();
             let csrc = root.join("hbbft_amd").join("csrc");
             for f in &["kernels.hip", "api.hip", "jit.hip", "wire.hip", "pairing.hip", "sim.hip",
-                       "device_common.hpp", "launchers.hpp", "jit.hpp", "bls_consts.hpp", "Makefile"] {
+                       "version.cpp", "device_common.hpp", "launchers.hpp", "jit.hpp",
+                       "bls_consts.hpp", "Makefile"] {
                 println!("cargo:rerun-if-changed={}", csrc.join(f).display());
             }
             println!("cargo:rerun-if-changed={}", root.join("include").join("hbrbc.h").display());

@@ -140,6 +140,10 @@ def lib():
         "hbrbc_pairing_check_prepared": (ctypes.c_int, [_P, _P, _S, _P, _P, _S, _P, _P, _P]),
         "hbrbc_pairing_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P, _P]),
         "hbrbc_pairing_check_batch": (ctypes.c_int, [_P, _P, _S, _P, _P, _P]),
+        "hbrbc_g1_prepared_size": (_S, [_S]),
+        "hbrbc_g1_prepare": (ctypes.c_int, [_P, _S, _P, _P]),
+        "hbrbc_pairing_check_prepared_keys": (ctypes.c_int, [_P, _P, _S, _P, _P, _S, _P, _P, _S, _P,
+                                                             _P, _P]),
         "hbrbc_pairing_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                                ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     }

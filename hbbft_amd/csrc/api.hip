@@ -2279,6 +2279,49 @@ int hbrbc_pairing_check_prepared(const uint8_t *g1, const void *prepared, size_t
     return HBRBC_OK;
 }
 
+size_t hbrbc_g1_prepared_size(size_t points) {
+    return round_up(g1_key_words(points) * 4, 256) + round_up(points, 256);
+}
+
+int hbrbc_g1_prepare(const uint8_t *g1, size_t count, void *prepared, void *stream) {
+    if (count == 0) return HBRBC_OK;
+    if (!g1 || !prepared) return fail(HBRBC_E_INVALID_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(HBRBC_E_NO_DEVICE, "no HIP device visible");
+    uint32_t *keys = static_cast<uint32_t *>(prepared);
+    uint8_t *kst = static_cast<uint8_t *>(prepared) + round_up(g1_key_words(count) * 4, 256);
+    HB_HIP(launch_g1_prepare(g1, count, keys, kst, static_cast<hipStream_t>(stream)));
+    return HBRBC_OK;
+}
+
+int hbrbc_pairing_check_prepared_keys(const uint8_t *g1_a, const void *keys, size_t key_points,
+                                      const uint32_t *idx_c, const void *prepared, size_t points,
+                                      const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
+                                      uint8_t *ok_out, void *workspace, void *stream) {
+    if (count == 0) return HBRBC_OK;
+    if (!g1_a || !keys || !idx_c || !prepared || !idx_b || !idx_d || !ok_out || !workspace)
+        return fail(HBRBC_E_INVALID_ARG, "null argument");
+    if (points == 0) return fail(HBRBC_E_INVALID_ARG, "no prepared points");
+    if (key_points == 0) return fail(HBRBC_E_INVALID_ARG, "no prepared keys");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(HBRBC_E_NO_DEVICE, "no HIP device visible");
+    const uint32_t *kw = static_cast<const uint32_t *>(keys);
+    const uint8_t *kst =
+        static_cast<const uint8_t *>(keys) + round_up(g1_key_words(key_points) * 4, 256);
+    const uint32_t *prep = static_cast<const uint32_t *>(prepared);
+    const uint8_t *pst =
+        static_cast<const uint8_t *>(prepared) + round_up(pairing_prepared_words(points) * 4, 256);
+    uint32_t *ws = static_cast<uint32_t *>(workspace);
+    uint8_t *st = static_cast<uint8_t *>(workspace) + round_up(count * 576, 256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HB_HIP(launch_pairing_miller_prepared_keys(g1_a, kw, kst, idx_c, key_points, prep, pst, idx_b,
+                                               idx_d, points, count, ws, st, s));
+    HB_HIP(launch_pairing_final(ws, count, count, 1, st, nullptr, ok_out, s));
+    return HBRBC_OK;
+}
+
 int hbrbc_pairing_check(const uint8_t a[96], const uint8_t b[192], const uint8_t c[96],
                         const uint8_t d[192], int *result) {
     if (!a || !b || !c || !d || !result) return fail(HBRBC_E_INVALID_ARG, "null argument");

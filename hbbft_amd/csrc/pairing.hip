@@ -1203,20 +1203,79 @@ NOINL void apply_prepared_in(Fp12 &f, const uint32_t *line, const Fp &xp, const 
 #define HB_APPLY_PREPARED apply_prepared
 #endif
 
+// Prepared G1 keys: hbbft checks every decryption share against the public
+// key share pk_i of its sender (threshold_decrypt.rs:220-228), and the
+// validator set's N key shares are the same for every ciphertext of an epoch
+// -- the crate holds them as curve points, so it decodes and checks them once,
+// not per share.  One lane per key: decoded and checked like any G1 input
+// (canonical coordinates, on the curve, order r), stored as Montgomery affine
+// x || y (kG1KeyWords words), status at kst[q] (0 ok, 1 infinity, 2 invalid).
+constexpr int kG1KeyWords = 2 * NL;
+
+DEV void load_g1_key(const uint32_t *src, Fp &x, Fp &y) {
+#pragma unroll
+    for (int w = 0; w < NL; w += 4) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(src + w);
+        const uint4 b = *reinterpret_cast<const uint4 *>(src + NL + w);
+        x.l[w] = a.x; x.l[w + 1] = a.y; x.l[w + 2] = a.z; x.l[w + 3] = a.w;
+        y.l[w] = b.x; y.l[w + 1] = b.y; y.l[w + 2] = b.z; y.l[w + 3] = b.w;
+    }
+}
+
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void g1_prepare_kernel(
+    const uint8_t *__restrict__ g1, size_t count, uint32_t *__restrict__ keys,
+    uint8_t *__restrict__ kst) {
+    const size_t q = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    if (q >= count) return;
+    Fp x, y;
+    const int st = decode_g1(g1 + q * 96, x, y);
+    if (st != PT_OK) {
+        fp_zero(x);
+        fp_zero(y);
+    }
+    uint32_t *dst = keys + q * kG1KeyWords;
+#pragma unroll
+    for (int w = 0; w < NL; w += 4) {
+        *reinterpret_cast<uint4 *>(dst + w) = make_uint4(x.l[w], x.l[w + 1], x.l[w + 2], x.l[w + 3]);
+        *reinterpret_cast<uint4 *>(dst + NL + w) = make_uint4(y.l[w], y.l[w + 1], y.l[w + 2], y.l[w + 3]);
+    }
+    kst[q] = (uint8_t)st;
+}
+
 // One lane per check e(a, b) == e(c, d) with b, d prepared (points ib[i],
 // id[i] of the table): g1 holds a, c at rows 2i, 2i+1.  Lanes of a wave
 // checking against the same points read the same lines (one cache line
 // serves the wave).
+// KEYS: c comes from a table of prepared G1 keys (g1_prepare_kernel) by
+// index ic[i] and g1 holds only a_0, a_1, ...; otherwise g1 holds a_0, c_0,
+// a_1, c_1, ... and both points of a check are decoded here.
+template <bool KEYS>
 __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void miller_prepared_kernel(
-    const uint8_t *__restrict__ g1, const uint32_t *__restrict__ prep,
+    const uint8_t *__restrict__ g1, const uint32_t *__restrict__ keys,
+    const uint8_t *__restrict__ kst, const uint32_t *__restrict__ ic, size_t nkeys,
+    const uint32_t *__restrict__ prep,
     const uint8_t *__restrict__ pst, const uint32_t *__restrict__ ib,
     const uint32_t *__restrict__ id, size_t points, size_t count, uint32_t *__restrict__ ws,
     uint8_t *__restrict__ status) {
     const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
     if (i >= count) return;
     Fp xa, ya, xc, yc;
-    const int sa = decode_g1(g1 + (2 * i) * 96, xa, ya);
-    const int sc = decode_g1(g1 + (2 * i + 1) * 96, xc, yc);
+    int sa, sc;
+    if constexpr (KEYS) {
+        sa = decode_g1(g1 + i * 96, xa, ya);
+        const uint32_t qc = ic[i];
+        // an index past the key table is an invalid input, never an out-of-bounds read
+        sc = qc < nkeys ? kst[qc] : PT_BAD;
+        if (sc == PT_OK) {
+            load_g1_key(keys + (size_t)qc * kG1KeyWords, xc, yc);
+        } else {
+            fp_zero(xc);
+            fp_zero(yc);
+        }
+    } else {
+        sa = decode_g1(g1 + (2 * i) * 96, xa, ya);
+        sc = decode_g1(g1 + (2 * i + 1) * 96, xc, yc);
+    }
     uint32_t qb = ib[i], qd = id[i];
     // an index past the table is an invalid input, never an out-of-bounds read
     const bool range_ok = qb < points && qd < points;
@@ -1373,8 +1432,34 @@ hipError_t launch_pairing_miller_prepared(const uint8_t *g1, const uint32_t *pre
     if (count == 0) return hipSuccess;
     if (points == 0) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
-    hipLaunchKernelGGL(miller_prepared_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, prep, pst,
-                       ib, id, points, count, ws, status);
+    hipLaunchKernelGGL(miller_prepared_kernel<false>, dim3(blocks), dim3(kPairBlock), 0, s, g1,
+                       nullptr, nullptr, nullptr, (size_t)0, prep, pst, ib, id, points, count, ws,
+                       status);
+    return hipGetLastError();
+}
+
+size_t g1_key_words(size_t points) { return points * (size_t)kG1KeyWords; }
+
+hipError_t launch_g1_prepare(const uint8_t *g1, size_t count, uint32_t *keys, uint8_t *kst,
+                             hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(g1_prepare_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g1, count, keys,
+                       kst);
+    return hipGetLastError();
+}
+
+hipError_t launch_pairing_miller_prepared_keys(const uint8_t *g1_a, const uint32_t *keys,
+                                               const uint8_t *kst, const uint32_t *ic,
+                                               size_t nkeys, const uint32_t *prep,
+                                               const uint8_t *pst, const uint32_t *ib,
+                                               const uint32_t *id, size_t points, size_t count,
+                                               uint32_t *ws, uint8_t *status, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (points == 0 || nkeys == 0) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL(miller_prepared_kernel<true>, dim3(blocks), dim3(kPairBlock), 0, s, g1_a,
+                       keys, kst, ic, nkeys, prep, pst, ib, id, points, count, ws, status);
     return hipGetLastError();
 }
 

@@ -124,12 +124,49 @@ def pairing_check_prepared(g1, prep, points, idx_b, idx_d, ws=None, stream=None)
     return ok
 
 
+def g1_prepare(g1, stream=None):
+    """Decode and check G1 points (uint8 [n, 96]) once -- hbbft's public key
+    shares pk_i, which the crate holds as curve points and does not decode per
+    share.  Returns the device table (uint8) for pairing_check_prepared_keys."""
+    torch = _torch()
+    n = g1.shape[0]
+    assert g1.shape == (n, G1_BYTES) and g1.is_contiguous()
+    keys = torch.empty(max(1, lib().hbrbc_g1_prepared_size(n)), dtype=torch.uint8,
+                       device=g1.device)
+    _check(lib().hbrbc_g1_prepare(g1.data_ptr(), n, keys.data_ptr(), _stream(g1.device, stream)))
+    return keys
+
+
+def pairing_check_prepared_keys(shares, keys, key_points, idx_c, prep, points, idx_b, idx_d,
+                                ws=None, stream=None):
+    """count checks e(a_i, P[idx_b[i]]) == e(K[idx_c[i]], P[idx_d[i]]): shares
+    uint8 [count, 96] = a_0, a_1, ...; K = `key_points` prepared G1 keys
+    (g1_prepare), P = `points` prepared G2 points (g2_prepare); idx_* int32
+    [count].  Returns uint8 [count]: 1 equal, 0 not, 2 invalid point or index."""
+    torch = _torch()
+    count = shares.shape[0]
+    assert shares.shape == (count, G1_BYTES) and shares.is_contiguous()
+    for t in (idx_b, idx_c, idx_d):
+        assert t.shape == (count,) and t.dtype == torch.int32 and t.is_contiguous()
+    ok = torch.empty((count,), dtype=torch.uint8, device=shares.device)
+    if ws is None:
+        ws = workspace(count, shares.device.index)
+    assert ws.numel() >= lib().hbrbc_pairing_workspace_size(count)
+    _check(lib().hbrbc_pairing_check_prepared_keys(
+        shares.data_ptr(), keys.data_ptr(), key_points, idx_c.data_ptr(), prep.data_ptr(), points,
+        idx_b.data_ptr(), idx_d.data_ptr(), count, ok.data_ptr(), ws.data_ptr(),
+        _stream(shares.device, stream)))
+    return ok
+
+
 def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
     """`verify_decryption_share` for many shares of a few ciphertexts, as
     ThresholdDecrypt receives them: ciphertexts = [(hash G2, W G2)], shares =
     [(ciphertext index, share G1, pk_share G1)].  Each ciphertext's H and W
-    are prepared once; shares are grouped by ciphertext so a wave shares its
-    lines.  Returns bools in the order of `shares`."""
+    are prepared once, each distinct key share pk_i is decoded and checked
+    once (the crate holds the validator set's key shares as points); shares
+    are grouped by ciphertext so a wave shares its lines.  Returns bools in
+    the order of `shares`."""
     import numpy as np
     torch = _torch()
     if not shares:
@@ -140,16 +177,23 @@ def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
         g2[2 * j] = np.frombuffer(h, np.uint8)
         g2[2 * j + 1] = np.frombuffer(w, np.uint8)
     prep = g2_prepare(torch.from_numpy(g2).to(dev))
+    key_ids = {}
+    for _, _, pk in shares:
+        key_ids.setdefault(bytes(pk), len(key_ids))
+    kt = np.stack([np.frombuffer(k, np.uint8) for k in key_ids])
+    ktab = g1_prepare(torch.from_numpy(kt).to(dev))
     order = sorted(range(len(shares)), key=lambda i: shares[i][0])
-    g1 = np.empty((2 * len(shares), G1_BYTES), np.uint8)
+    g1 = np.empty((len(shares), G1_BYTES), np.uint8)
     ib = np.empty(len(shares), np.int32)
+    ic = np.empty(len(shares), np.int32)
     for r, i in enumerate(order):
         ct, share, pk = shares[i]
-        g1[2 * r] = np.frombuffer(share, np.uint8)
-        g1[2 * r + 1] = np.frombuffer(pk, np.uint8)
+        g1[r] = np.frombuffer(share, np.uint8)
         ib[r] = 2 * ct
-    ok = pairing_check_prepared(torch.from_numpy(g1).to(dev), prep, 2 * len(ciphertexts),
-                                torch.from_numpy(ib).to(dev), torch.from_numpy(ib + 1).to(dev))
+        ic[r] = key_ids[bytes(pk)]
+    ok = pairing_check_prepared_keys(torch.from_numpy(g1).to(dev), ktab, len(key_ids),
+                                     torch.from_numpy(ic).to(dev), prep, 2 * len(ciphertexts),
+                                     torch.from_numpy(ib).to(dev), torch.from_numpy(ib + 1).to(dev))
     okh = ok.cpu().tolist()
     out = [False] * len(shares)
     for r, i in enumerate(order):

@@ -465,6 +465,25 @@ int hbrbc_g2_prepare(const uint8_t *g2, size_t count, void *prepared, void *stre
 int hbrbc_pairing_check_prepared(const uint8_t *g1, const void *prepared, size_t points,
                                  const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
                                  uint8_t *ok_out, void *workspace, void *stream);
+/* Prepared G1 keys: hbbft checks each decryption share against its sender's
+ * public key share pk_i, and the validator set's key shares are the same for
+ * every ciphertext; `threshold_crypto` holds them as curve points, decoded and
+ * checked once.  hbrbc_g1_prepare decodes and checks `count` G1 points once
+ * (as any G1 input: canonical, on the curve, order r) into `prepared` >=
+ * hbrbc_g1_prepared_size(count) bytes of device memory; an invalid point is
+ * marked there and fails every check that uses it.  Device memory, async. */
+size_t hbrbc_g1_prepared_size(size_t points);
+int hbrbc_g1_prepare(const uint8_t *g1, size_t count, void *prepared, void *stream);
+/* count checks e(a_i, P[idx_b[i]]) == e(K[idx_c[i]], P[idx_d[i]]) with K the
+ * `key_points` prepared G1 keys and P the `points` prepared G2 points: g1_a
+ * holds a_0, a_1, ... (count points); ok_out as hbrbc_pairing_check_batch
+ * (an index past either table makes that check 2).  For
+ * verify_decryption_share: a = share, K = the pk_i table, b = hash, d = W.
+ * workspace >= hbrbc_pairing_workspace_size(count).  Device memory, async. */
+int hbrbc_pairing_check_prepared_keys(const uint8_t *g1_a, const void *keys, size_t key_points,
+                                      const uint32_t *idx_c, const void *prepared, size_t points,
+                                      const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
+                                      uint8_t *ok_out, void *workspace, void *stream);
 /* Per-call shim on host memory (one check, synchronous, current device):
  * *result = 1 if e(a, b) == e(c, d), 0 if not; HBRBC_E_INVALID_ARG for an
  * invalid point. */

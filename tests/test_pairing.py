@@ -203,6 +203,63 @@ def test_prepared_checks_match_plain_checks():
     assert T.pairing_check_prepared(g1, prep, 3, ib2, idd).cpu().tolist() == [1, 2, 2, 1]
 
 
+def test_prepared_keys_match_prepared_checks():
+    """Checks against a table of prepared G1 keys (hbbft's pk_i, decoded and
+    checked once) give exactly the outcomes of the same checks with both G1
+    points decoded per check: valid and tampered shares, keys that are
+    infinity, off the subgroup or non-canonical, and indices past either
+    table (as uint32: -1 is 2^32-1), which are invalid inputs, not reads."""
+    import torch
+    from hbbft_amd import threshold as T
+    rng = random.Random(33)
+    cts, rows = [], []
+    keys_sk = [rng.randrange(1, B.R) for _ in range(6)]
+    keys = [B.g1_bytes(B.g1_mul(B.G1_GEN, sk)) for sk in keys_sk]
+    (p0, _), _ = _off_subgroup_points()
+    noncanon = bytearray(B.g1_bytes(B.g1_mul(B.G1_GEN, 3)))
+    noncanon[0] = (noncanon[0] & 0xE0) | 0x1F   # x >= p (p's top byte is 0x1a; flags kept)
+    keys += [B.g1_bytes(None), B.g1_bytes(p0), bytes(noncanon)]   # keys 6, 7, 8
+    for j in range(2):
+        h, r_enc = rng.randrange(1, B.R), rng.randrange(1, B.R)
+        H = B.g2_mul(B.G2_GEN, h)
+        U = B.g1_mul(B.G1_GEN, r_enc)
+        W = B.g2_mul(H, r_enc)
+        cts += [B.g2_bytes(H), B.g2_bytes(W)]
+        for i in range(len(keys)):
+            share = B.g1_mul(U, keys_sk[i] if i < 6 else 5)
+            if (i + j) % 4 == 1:
+                share = B.g1_add(share, B.G1_GEN)   # tampered
+            rows.append((B.g1_bytes(share), i, 2 * j, 2 * j + 1))
+    rows.append((rows[0][0], 9, 0, 1))            # key index past the table
+    rows.append((rows[0][0], -1, 0, 1))
+    rows.append((rows[0][0], 0, 4, 1))            # G2 index past the table
+    prep = T.g2_prepare(_t(cts, 192))
+    ktab = T.g1_prepare(_t(keys, 96))
+    dev = "cuda:0"
+    ib = torch.tensor([r[2] for r in rows], dtype=torch.int32, device=dev)
+    idd = torch.tensor([r[3] for r in rows], dtype=torch.int32, device=dev)
+    ic = torch.tensor([r[1] for r in rows], dtype=torch.int32, device=dev)
+    got = T.pairing_check_prepared_keys(_t([r[0] for r in rows], 96), ktab, len(keys), ic, prep,
+                                        len(cts), ib, idd).cpu().tolist()
+    # the same checks with the key decoded per check (the key index clamped
+    # for the rows whose index is out of range: their outcome must be 2)
+    g1 = _t([x for r in rows for x in (r[0], keys[r[1] if 0 <= r[1] < len(keys) else 0])], 96)
+    ref = T.pairing_check_prepared(g1, prep, len(cts), ib, idd).cpu().tolist()
+    n = len(rows)
+    assert got[:n - 3] == ref[:n - 3] and got[n - 3:] == [2, 2, 2]
+    assert ref[n - 1] == 2
+    # valid keys: 1 unless tampered; invalid keys (infinity on one side gives 1
+    # against a non-1 value, off-subgroup and non-canonical are invalid)
+    for r, v in zip(rows[:n - 3], got[:n - 3]):
+        i, j = r[1], r[2] // 2
+        if i < 6:
+            assert v == (0 if (i + j) % 4 == 1 else 1), (i, j, v)
+        elif i == 6:
+            assert v == 0
+        else:
+            assert v == 2
+
+
 def _off_subgroup_points():
     """On-curve points outside the order-r subgroups (the crate's into_affine
     rejects them): a plain curve point of E / E', and a subgroup point plus a

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--prepared", action="store_true",
                     help="grouped checks against prepared G2 points (64 shares per ciphertext)")
+    ap.add_argument("--keys", type=int, default=1,
+                    help="with --prepared: 1 = key shares pk_i from a prepared G1 table (the "
+                         "bench's f4 leg), 0 = decoded per check")
     a = ap.parse_args()
     if a.prepared:
         return prepared(a)
@@ -88,10 +91,20 @@ def prepared(a):
     ib = torch.arange(a.n, dtype=torch.int32, device="cuda") // 64 * 2
     idd = ib + 1
     ws = T.workspace(a.n)
+    shares = d1[0::2].contiguous()
+    keys_h = np.stack([np.frombuffer(bytes.fromhex(sh["pk"]), np.uint8)
+                       for grp in groups for sh in grp["shares"]])
+    dkeys = torch.from_numpy(keys_h).cuda()
+    ic = torch.from_numpy(np.array([(q % len(groups)) * 64 + s for q in range(ng)
+                                    for s in range(64)], np.int32)).cuda()
 
     def run():
         prep = T.g2_prepare(d2)
-        return T.pairing_check_prepared(d1, prep, 2 * ng, ib, idd, ws)
+        if not a.keys:
+            return T.pairing_check_prepared(d1, prep, 2 * ng, ib, idd, ws)
+        keys = T.g1_prepare(dkeys)
+        return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], ic, prep, 2 * ng, ib,
+                                             idd, ws)
     ok = run()
     torch.cuda.synchronize()
     assert ok.cpu().tolist() == expect, "check outcomes differ from the fixtures"
@@ -102,7 +115,8 @@ def prepared(a):
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     t = sorted(times)[len(times) // 2]
-    print(json.dumps({"n_checks": a.n, "mode": "prepared", "groups": ng, "ms": t * 1e3,
+    print(json.dumps({"n_checks": a.n, "mode": "prepared" + ("+keys" if a.keys else ""),
+                      "groups": ng, "ms": t * 1e3,
                       "checks_per_s": a.n / t, "outcomes_exact": True}), flush=True)
 
 

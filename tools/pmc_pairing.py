@@ -16,7 +16,8 @@ def main():
     for f in glob.glob(d + "/pmc/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             k = row.get("Kernel_Name", "")
-            kern = ("prepare" if "g2_prepare" in k else "miller" if "miller" in k
+            kern = ("prepare" if "g2_prepare" in k else "prepare_keys" if "g1_prepare" in k
+                    else "miller" if "miller" in k
                     else "final_exp" if "final_exp_kernel" in k else None)
             if kern:
                 vals[kern][row["Counter_Name"]].append(float(row["Counter_Value"]))
@@ -28,7 +29,8 @@ def main():
     for f in glob.glob(d + "/trace/**/*kernel_stats.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             k = row["Name"]
-            kern = ("prepare" if "g2_prepare" in k else "miller" if "miller" in k
+            kern = ("prepare" if "g2_prepare" in k else "prepare_keys" if "g1_prepare" in k
+                    else "miller" if "miller" in k
                     else "final_exp" if "final_exp_kernel" in k else None)
             if kern:
                 stats[kern] = float(row["AverageNs"]) / 1e6
