@@ -8,8 +8,17 @@ of `count` independent broadcast instances already resident in HBM:
   decode_from_shards with f random erasures per instance (563-601: decode
   matrix + reconstruct, re-tree, root compare, unframe).
 value = payload bytes of every instance on every rank / max-over-ranks wall
-time of the K timed steps (GB/s, 1e9).  Multi-GPU: instances are sharded
-across ranks with no data-path collective (weak scaling).
+time of the K timed steps (GB/s, 1e9), without the HIP-event-timed erase fill
+that stands in for transport (value_incl_erase keeps it).  Multi-GPU:
+instances are sharded across ranks with no data-path collective (weak
+scaling).
+
+Rank 0 prints ONE compact JSON line of at most LINE_CAP bytes (the driver
+keeps the last ~8 KB of stdout): the contract's fields, the dominant kernel's
+roofline, the CPU baseline and each object's rate; --detail PATH writes the
+full record.  Objects run in order -- headline, cfg2, cfg5, f4, then the
+validator-sharded ones -- each secondary one guarded and under a deadline
+(Phases), so a failure or a stuck collective costs only that object.
 
 Validator-sharded simulation (the `validators` object of the same line, or
 the headline with --mode validators): the N validators are split over the
