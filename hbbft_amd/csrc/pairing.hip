@@ -315,13 +315,21 @@ DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
 }
 
 #else
+// HB_FP2_SERIAL (A/B): a scheduling barrier between the three Fp products, so
+// the scheduler cannot interleave them (fewer live digits, less ILP)
+#ifndef HB_FP2_SERIAL
+#define HB_FP2_SERIAL 0
+#endif
 DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     Fp t0, t1, s0, s1;
     fp_mul(t0, a.c0, b.c0);
+    if (HB_FP2_SERIAL) __builtin_amdgcn_sched_barrier(0);
     fp_mul(t1, a.c1, b.c1);
+    if (HB_FP2_SERIAL) __builtin_amdgcn_sched_barrier(0);
     fp_add(s0, a.c0, a.c1);
     fp_add(s1, b.c0, b.c1);
     fp_mul(s0, s0, s1);
+    if (HB_FP2_SERIAL) __builtin_amdgcn_sched_barrier(0);
     fp_sub(r.c0, t0, t1);
     fp_sub(s0, s0, t0);
     fp_sub(r.c1, s0, t1);
