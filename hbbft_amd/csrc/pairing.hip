@@ -318,7 +318,7 @@ DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
 // HB_FP2_SERIAL (A/B): a scheduling barrier between the three Fp products, so
 // the scheduler cannot interleave them (fewer live digits, less ILP)
 #ifndef HB_FP2_SERIAL
-#define HB_FP2_SERIAL 0
+#define HB_FP2_SERIAL 1   // round 6: Miller 71.1 -> 66.8, final exp 68.8 -> 66.8 ms (r6u)
 #endif
 DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     Fp t0, t1, s0, s1;
@@ -626,10 +626,17 @@ NOINL void fp12_frob(Fp12 &r, const Fp12 &a, int k) {
 }
 
 // (a + b s)^2 in Fp4 = Fp2[s]/(s^2 - xi): (a^2 + xi b^2, 2ab)
+// HB_CYC_SERIAL (A/B): scheduling barriers between the Fp2 squarings of the
+// cyclotomic square (fewer live digits, less ILP)
+#ifndef HB_CYC_SERIAL
+#define HB_CYC_SERIAL 0
+#endif
 DEV void fp4_sqr(Fp2 &c0, Fp2 &c1, const Fp2 &a, const Fp2 &b) {
     Fp2 t0, t1, t2;
     fp2_sqr_in(t0, a);
+    if (HB_CYC_SERIAL) __builtin_amdgcn_sched_barrier(0);
     fp2_sqr_in(t1, b);
+    if (HB_CYC_SERIAL) __builtin_amdgcn_sched_barrier(0);
     fp2_mul_xi(t2, t1);
     fp2_add(c0, t2, t0);
     fp2_add(t2, a, b);
