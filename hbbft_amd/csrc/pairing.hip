@@ -693,7 +693,7 @@ void fp12_cyclo_sqr(Fp12 &f) {
 // HB_EXPX_INL (A/B): 1 = the five products by `a` inlined too (Fp6 products
 // inlined), so the whole f^|x| is one unit with no call inside its loop
 #ifndef HB_EXPX_INL
-#define HB_EXPX_INL 0
+#define HB_EXPX_INL 1   // round 6, on the serialised Fp2 base: final exp 66.9 -> 59.1 ms (r6z)
 #endif
 NOINL void fp12_exp_by_x(Fp12 &r, const Fp12 &a, int shift) {
     const uint64_t e = kXAbs >> shift;
