@@ -1217,6 +1217,22 @@ NOINL void apply_prepared_in(Fp12 &f, const uint32_t *line, const Fp &xp, const 
 #else
 #define HB_APPLY_PREPARED apply_prepared
 #endif
+// HB_MILLER_INL 3: the whole bit step -- the squaring and both line
+// applications -- as one unit, so f does not pass through the stack between
+// them
+DEV void apply_prepared_body(Fp12 &f, const uint32_t *line, const Fp &xp, const Fp &yp) {
+    Fp2 l0, l1, l4, a, b;
+    load_line(line, l0, l1, l4);
+    fp2_mul_fp(a, l1, xp);
+    fp2_mul_fp(b, l4, yp);
+    fp12_mul_by_014_in(f, l0, a, b);
+}
+NOINL void miller_step(Fp12 &f, const uint32_t *p1, const uint32_t *p2, const Fp &xa,
+                       const Fp &ya, const Fp &xc, const Fp &yc, bool on1, bool on2) {
+    fp12_sqr_t<true>(f, f);
+    if (on1) apply_prepared_body(f, p1, xa, ya);
+    if (on2) apply_prepared_body(f, p2, xc, yc);
+}
 
 // Prepared G1 keys: hbbft checks every decryption share against the public
 // key share pk_i of its sender (threshold_decrypt.rs:220-228), and the
@@ -1306,9 +1322,13 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_P
         const uint32_t *p1 = prep + (size_t)qb * kLines * kLineWords;
         const uint32_t *p2 = prep + (size_t)qd * kLines * kLineWords;
         for (int b = 62; b >= 0; --b) {
-            if (HB_MILLER_INL) miller_sqr(f); else fp12_sqr(f, f);
-            if (on1) HB_APPLY_PREPARED(f, p1, xa, ya);
-            if (on2) HB_APPLY_PREPARED(f, p2, xc, yc);
+            if (HB_MILLER_INL >= 3) {
+                miller_step(f, p1, p2, xa, ya, xc, yc, on1, on2);
+            } else {
+                if (HB_MILLER_INL) miller_sqr(f); else fp12_sqr(f, f);
+                if (on1) HB_APPLY_PREPARED(f, p1, xa, ya);
+                if (on2) HB_APPLY_PREPARED(f, p2, xc, yc);
+            }
             p1 += kLineWords;
             p2 += kLineWords;
             if ((kXAbs >> b) & 1u) {
