@@ -320,20 +320,22 @@ DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
 #ifndef HB_FP2_SERIAL
 #define HB_FP2_SERIAL 1   // round 6: Miller 71.1 -> 66.8, final exp 68.8 -> 66.8 ms (r6u)
 #endif
-DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+template <bool SER>
+DEV void fp2_mul_t(Fp2 &r, const Fp2 &a, const Fp2 &b) {
     Fp t0, t1, s0, s1;
     fp_mul(t0, a.c0, b.c0);
-    if (HB_FP2_SERIAL) __builtin_amdgcn_sched_barrier(0);
+    if (SER) __builtin_amdgcn_sched_barrier(0);
     fp_mul(t1, a.c1, b.c1);
-    if (HB_FP2_SERIAL) __builtin_amdgcn_sched_barrier(0);
+    if (SER) __builtin_amdgcn_sched_barrier(0);
     fp_add(s0, a.c0, a.c1);
     fp_add(s1, b.c0, b.c1);
     fp_mul(s0, s0, s1);
-    if (HB_FP2_SERIAL) __builtin_amdgcn_sched_barrier(0);
+    if (SER) __builtin_amdgcn_sched_barrier(0);
     fp_sub(r.c0, t0, t1);
     fp_sub(s0, s0, t0);
     fp_sub(r.c1, s0, t1);
 }
+DEV void fp2_mul_in(Fp2 &r, const Fp2 &a, const Fp2 &b) { fp2_mul_t<HB_FP2_SERIAL != 0>(r, a, b); }
 
 #endif
 
@@ -713,32 +715,46 @@ struct G2Proj { Fp2 x, y, z; };
 // T <- 2T and the tangent line at T before it is evaluated at P, scaled by
 // 2YZ^2: L0 + (L1 xp) v + (L4 yp) v w with L0 = 3X^3 - 2Y^2 Z, L1 = -3X^2 Z,
 // L4 = 2 Y Z^2.
+// HB_G2_SERIAL (A/B): the serialised Fp2 product in the G2 line units too
+// (G2 preparation: one lane per point, latency-bound at 1/16 of the wave
+// slots, where the serialisation only lengthens the chain)
+#ifndef HB_G2_SERIAL
+#define HB_G2_SERIAL 1
+#endif
+DEV void fp2_mul_g2(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+#if HB_LAZY_MUL
+    fp2_mul_in(r, a, b);
+#else
+    fp2_mul_t<HB_G2_SERIAL != 0>(r, a, b);
+#endif
+}
+
 NOINL void g2_dbl_line(G2Proj &T, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
     Fp2 xx, w, s, ss, sss, rr, RR, B, h, t;
     fp2_sqr_in(xx, T.x);
     fp2_dbl(w, xx);
     fp2_add(w, w, xx);            // w = 3 X^2
-    fp2_mul_in(s, T.y, T.z);
+    fp2_mul_g2(s, T.y, T.z);
     fp2_dbl(s, s);                // s = 2 Y Z
     fp2_sqr_in(ss, s);
-    fp2_mul_in(sss, s, ss);
-    fp2_mul_in(rr, T.y, s);       // R = Y s = 2 Y^2 Z
+    fp2_mul_g2(sss, s, ss);
+    fp2_mul_g2(rr, T.y, s);       // R = Y s = 2 Y^2 Z
     fp2_sqr_in(RR, rr);
     fp2_add(B, T.x, rr);
     fp2_sqr_in(B, B);
     fp2_sub(B, B, xx);
     fp2_sub(B, B, RR);            // B = (X + R)^2 - X^2 - R^2
-    fp2_mul_in(l0, T.x, w);
+    fp2_mul_g2(l0, T.x, w);
     fp2_sub(l0, l0, rr);          // 3X^3 - 2Y^2 Z
-    fp2_mul_in(l1, w, T.z);
+    fp2_mul_g2(l1, w, T.z);
     fp2_neg(l1, l1);              // -3X^2 Z
-    fp2_mul_in(l4, s, T.z);       // 2 Y Z^2
+    fp2_mul_g2(l4, s, T.z);       // 2 Y Z^2
     fp2_sqr_in(h, w);
     fp2_sub(h, h, B);
     fp2_sub(h, h, B);             // h = w^2 - 2B
-    fp2_mul_in(T.x, h, s);
+    fp2_mul_g2(T.x, h, s);
     fp2_sub(t, B, h);
-    fp2_mul_in(t, w, t);
+    fp2_mul_g2(t, w, t);
     fp2_dbl(RR, RR);
     fp2_sub(T.y, t, RR);          // w (B - h) - 2 R^2
     T.z = sss;
@@ -749,30 +765,30 @@ NOINL void g2_dbl_line(G2Proj &T, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
 // v = xq Z - X.
 NOINL void g2_add_line(G2Proj &T, const Fp2 &xq, const Fp2 &yq, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
     Fp2 u, v, uu, vv, vvv, R, A, t;
-    fp2_mul_in(u, yq, T.z);
+    fp2_mul_g2(u, yq, T.z);
     fp2_sub(u, u, T.y);
-    fp2_mul_in(v, xq, T.z);
+    fp2_mul_g2(v, xq, T.z);
     fp2_sub(v, v, T.x);
-    fp2_mul_in(l0, u, xq);
-    fp2_mul_in(t, v, yq);
+    fp2_mul_g2(l0, u, xq);
+    fp2_mul_g2(t, v, yq);
     fp2_sub(l0, l0, t);
     fp2_neg(l1, u);
     l4 = v;
     fp2_sqr_in(uu, u);
     fp2_sqr_in(vv, v);
-    fp2_mul_in(vvv, v, vv);
-    fp2_mul_in(R, vv, T.x);
-    fp2_mul_in(A, uu, T.z);
+    fp2_mul_g2(vvv, v, vv);
+    fp2_mul_g2(R, vv, T.x);
+    fp2_mul_g2(A, uu, T.z);
     fp2_sub(A, A, vvv);
     fp2_sub(A, A, R);
     fp2_sub(A, A, R);             // A = uu Z - vvv - 2R
-    fp2_mul_in(T.x, v, A);
+    fp2_mul_g2(T.x, v, A);
     fp2_sub(t, R, A);
-    fp2_mul_in(t, u, t);
-    fp2_mul_in(vvv, vvv, T.y);
+    fp2_mul_g2(t, u, t);
+    fp2_mul_g2(vvv, vvv, T.y);
     fp2_sub(T.y, t, vvv);
-    fp2_mul_in(T.z, T.z, vv);
-    fp2_mul_in(T.z, T.z, v);      // Z vvv
+    fp2_mul_g2(T.z, T.z, vv);
+    fp2_mul_g2(T.z, T.z, v);      // Z vvv
 }
 
 // f <- f * line(P): the line evaluated at P = (xp, yp) (sparse (c0, c1, c4))
