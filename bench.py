@@ -1158,10 +1158,11 @@ def run_threshold(args, rank, world, dev):
     """f4 leg: F4_CHECKS verify_decryption_share checks per GPU per step in
     hbbft's shape -- groups of 64 shares checked against one ciphertext's H and
     W (threshold_decrypt.rs:204-229) -- e(share, H) == e(pk_i, W): every step
-    prepares each ciphertext's H and W (hbrbc_g2_prepare) and the key shares
-    pk_i (hbrbc_g1_prepare: decoded and checked once, as the crate holds them
-    as points), and checks the shares against them
-    (hbrbc_pairing_check_prepared_keys).  Inputs tile the 4
+    prepares each ciphertext's H and W (hbrbc_g2_prepare), decodes and checks
+    the key shares pk_i (hbrbc_g1_prepare: once, as the crate holds them as
+    points) and the received shares (hbrbc_g1_prepare, beside the G2
+    preparation on a side stream), and checks the shares against them
+    (hbrbc_pairing_check_prepared_pts).  Inputs tile the 4
     committed fixture groups (tests/golden/bls_vectors.json, one share in
     eight tampered); outcomes are checked exactly after warm-up.  The plain
     per-check form (hbrbc_pairing_check_batch) is timed beside it."""
@@ -1201,23 +1202,34 @@ def run_threshold(args, rank, world, dev):
     ws = T.workspace(n, dev.index)
     stream = torch.cuda.current_stream(dev)
 
-    # the two preparations fill few SIMDs (one lane per point: 8192 G2 points,
-    # 256 keys): the keys go on a side stream beside the G2 points
-    side = torch.cuda.Stream(dev) if os.environ.get("HBRBC_BENCH_F4_SIDE", "1") == "1" else None
+    # the G2 preparation fills few SIMDs (one lane per point: 8192 points, a
+    # serial chain each): the key shares and the received shares are decoded
+    # and checked (order r) on a side stream beside it, and the Miller loops
+    # only load them (hbrbc_pairing_check_prepared_pts).  HBRBC_BENCH_F4_SIDE:
+    # 2 (default) keys and shares beside the G2 points, 1 keys only (shares
+    # decoded inside the Miller kernel), 0 everything in order on one stream.
+    mode = int(os.environ.get("HBRBC_BENCH_F4_SIDE", "2"))
+    side = torch.cuda.Stream(dev) if mode > 0 else None
 
     def step():
-        if side is not None:
-            side.wait_stream(stream)
-            with torch.cuda.stream(side):
-                keys = T.g1_prepare(dkeys)
-            prep = T.g2_prepare(d2)
-            stream.wait_stream(side)
-            keys.record_stream(stream)
-        else:
+        if side is None:
             prep = T.g2_prepare(d2)
             keys = T.g1_prepare(dkeys)
-        return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng, ib,
-                                             idd, ws)
+            return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
+                                                 ib, idd, ws)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            keys = T.g1_prepare(dkeys)
+            sprep = T.g1_prepare(shares) if mode >= 2 else None
+        prep = T.g2_prepare(d2)
+        stream.wait_stream(side)
+        keys.record_stream(stream)
+        if sprep is None:
+            return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
+                                                 ib, idd, ws)
+        sprep.record_stream(stream)
+        return T.pairing_check_prepared_pts(sprep, n, keys, dkeys.shape[0], dic, prep, 2 * ng, ib,
+                                            idd, ws)
     for _ in range(max(1, args.warmup)):
         ok = step()
     torch.cuda.synchronize(dev)

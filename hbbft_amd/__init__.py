@@ -144,6 +144,8 @@ def lib():
         "hbrbc_g1_prepare": (ctypes.c_int, [_P, _S, _P, _P]),
         "hbrbc_pairing_check_prepared_keys": (ctypes.c_int, [_P, _P, _S, _P, _P, _S, _P, _P, _S, _P,
                                                              _P, _P]),
+        "hbrbc_pairing_check_prepared_pts": (ctypes.c_int, [_P, _P, _S, _P, _P, _S, _P, _P, _S, _P,
+                                                            _P, _P]),
         "hbrbc_pairing_check": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                                ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     }

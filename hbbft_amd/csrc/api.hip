@@ -2322,6 +2322,36 @@ int hbrbc_pairing_check_prepared_keys(const uint8_t *g1_a, const void *keys, siz
     return HBRBC_OK;
 }
 
+int hbrbc_pairing_check_prepared_pts(const void *a_prepared, const void *keys, size_t key_points,
+                                     const uint32_t *idx_c, const void *prepared, size_t points,
+                                     const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
+                                     uint8_t *ok_out, void *workspace, void *stream) {
+    if (count == 0) return HBRBC_OK;
+    if (!a_prepared || !keys || !idx_c || !prepared || !idx_b || !idx_d || !ok_out || !workspace)
+        return fail(HBRBC_E_INVALID_ARG, "null argument");
+    if (points == 0) return fail(HBRBC_E_INVALID_ARG, "no prepared points");
+    if (key_points == 0) return fail(HBRBC_E_INVALID_ARG, "no prepared keys");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(HBRBC_E_NO_DEVICE, "no HIP device visible");
+    const uint32_t *aw = static_cast<const uint32_t *>(a_prepared);
+    const uint8_t *ast =
+        static_cast<const uint8_t *>(a_prepared) + round_up(g1_key_words(count) * 4, 256);
+    const uint32_t *kw = static_cast<const uint32_t *>(keys);
+    const uint8_t *kst =
+        static_cast<const uint8_t *>(keys) + round_up(g1_key_words(key_points) * 4, 256);
+    const uint32_t *prep = static_cast<const uint32_t *>(prepared);
+    const uint8_t *pst =
+        static_cast<const uint8_t *>(prepared) + round_up(pairing_prepared_words(points) * 4, 256);
+    uint32_t *ws = static_cast<uint32_t *>(workspace);
+    uint8_t *st = static_cast<uint8_t *>(workspace) + round_up(count * 576, 256);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HB_HIP(launch_pairing_miller_prepared_pts(aw, ast, kw, kst, idx_c, key_points, prep, pst, idx_b,
+                                              idx_d, points, count, ws, st, s));
+    HB_HIP(launch_pairing_final(ws, count, count, 1, st, nullptr, ok_out, s));
+    return HBRBC_OK;
+}
+
 int hbrbc_pairing_check(const uint8_t a[96], const uint8_t b[192], const uint8_t c[96],
                         const uint8_t d[192], int *result) {
     if (!a || !b || !c || !d || !result) return fail(HBRBC_E_INVALID_ARG, "null argument");

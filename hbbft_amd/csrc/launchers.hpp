@@ -251,6 +251,13 @@ hipError_t launch_pairing_miller_prepared(const uint8_t *g1, const uint32_t *pre
                                           const uint32_t *id, size_t points, size_t count,
                                           uint32_t *ws, uint8_t *status, hipStream_t s);
 size_t g1_key_words(size_t points);
+hipError_t launch_pairing_miller_prepared_pts(const uint32_t *atab, const uint8_t *ast,
+                                              const uint32_t *keys, const uint8_t *kst,
+                                              const uint32_t *ic, size_t nkeys,
+                                              const uint32_t *prep, const uint8_t *pst,
+                                              const uint32_t *ib, const uint32_t *id,
+                                              size_t points, size_t count, uint32_t *ws,
+                                              uint8_t *status, hipStream_t s);
 hipError_t launch_g1_prepare(const uint8_t *g1, size_t count, uint32_t *keys, uint8_t *kst,
                              hipStream_t s);
 hipError_t launch_pairing_miller_prepared_keys(const uint8_t *g1_a, const uint32_t *keys,

@@ -1296,20 +1296,29 @@ __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_P
 // KEYS: c comes from a table of prepared G1 keys (g1_prepare_kernel) by
 // index ic[i] and g1 holds only a_0, a_1, ...; otherwise g1 holds a_0, c_0,
 // a_1, c_1, ... and both points of a check are decoded here.
-template <bool KEYS>
+// PTS (with KEYS): a also comes decoded, from a g1_prepare table of the
+// `count` shares (entry i, statuses `ast`), so the share decoding -- an
+// order-r check each -- runs as its own launch beside the G2 preparation.
+template <bool KEYS, bool PTS = false>
 __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void miller_prepared_kernel(
     const uint8_t *__restrict__ g1, const uint32_t *__restrict__ keys,
     const uint8_t *__restrict__ kst, const uint32_t *__restrict__ ic, size_t nkeys,
     const uint32_t *__restrict__ prep,
     const uint8_t *__restrict__ pst, const uint32_t *__restrict__ ib,
     const uint32_t *__restrict__ id, size_t points, size_t count, uint32_t *__restrict__ ws,
-    uint8_t *__restrict__ status) {
+    uint8_t *__restrict__ status, const uint32_t *__restrict__ atab = nullptr,
+    const uint8_t *__restrict__ ast = nullptr) {
     const size_t i = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
     if (i >= count) return;
     Fp xa, ya, xc, yc;
     int sa, sc;
     if constexpr (KEYS) {
-        sa = decode_g1(g1 + i * 96, xa, ya);
+        if constexpr (PTS) {
+            sa = ast[i];
+            load_g1_key(atab + i * kG1KeyWords, xa, ya);   // zeros unless the point is valid
+        } else {
+            sa = decode_g1(g1 + i * 96, xa, ya);
+        }
         const uint32_t qc = ic[i];
         // an index past the key table is an invalid input, never an out-of-bounds read
         sc = qc < nkeys ? kst[qc] : PT_BAD;
@@ -1490,6 +1499,22 @@ hipError_t launch_pairing_miller_prepared(const uint8_t *g1, const uint32_t *pre
 }
 
 size_t g1_key_words(size_t points) { return points * (size_t)kG1KeyWords; }
+
+hipError_t launch_pairing_miller_prepared_pts(const uint32_t *atab, const uint8_t *ast,
+                                              const uint32_t *keys, const uint8_t *kst,
+                                              const uint32_t *ic, size_t nkeys,
+                                              const uint32_t *prep, const uint8_t *pst,
+                                              const uint32_t *ib, const uint32_t *id,
+                                              size_t points, size_t count, uint32_t *ws,
+                                              uint8_t *status, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (points == 0 || nkeys == 0) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    hipLaunchKernelGGL((miller_prepared_kernel<true, true>), dim3(blocks), dim3(kPairBlock), 0, s,
+                       nullptr, keys, kst, ic, nkeys, prep, pst, ib, id, points, count, ws, status,
+                       atab, ast);
+    return hipGetLastError();
+}
 
 hipError_t launch_g1_prepare(const uint8_t *g1, size_t count, uint32_t *keys, uint8_t *kst,
                              hipStream_t s) {

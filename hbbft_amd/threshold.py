@@ -159,6 +159,27 @@ def pairing_check_prepared_keys(shares, keys, key_points, idx_c, prep, points, i
     return ok
 
 
+def pairing_check_prepared_pts(a_prep, count, keys, key_points, idx_c, prep, points, idx_b, idx_d,
+                               ws=None, stream=None):
+    """pairing_check_prepared_keys with the shares decoded beforehand:
+    a_prep = g1_prepare(shares) over the `count` shares (a_i = entry i), so
+    their decoding can run as its own launch (e.g. beside g2_prepare on
+    another stream).  Returns uint8 [count] as pairing_check_prepared_keys."""
+    torch = _torch()
+    for t in (idx_b, idx_c, idx_d):
+        assert t.shape == (count,) and t.dtype == torch.int32 and t.is_contiguous()
+    assert a_prep.numel() >= lib().hbrbc_g1_prepared_size(count)
+    ok = torch.empty((count,), dtype=torch.uint8, device=a_prep.device)
+    if ws is None:
+        ws = workspace(count, a_prep.device.index)
+    assert ws.numel() >= lib().hbrbc_pairing_workspace_size(count)
+    _check(lib().hbrbc_pairing_check_prepared_pts(
+        a_prep.data_ptr(), keys.data_ptr(), key_points, idx_c.data_ptr(), prep.data_ptr(), points,
+        idx_b.data_ptr(), idx_d.data_ptr(), count, ok.data_ptr(), ws.data_ptr(),
+        _stream(a_prep.device, stream)))
+    return ok
+
+
 def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
     """`verify_decryption_share` for many shares of a few ciphertexts, as
     ThresholdDecrypt receives them: ciphertexts = [(hash G2, W G2)], shares =

@@ -484,6 +484,15 @@ int hbrbc_pairing_check_prepared_keys(const uint8_t *g1_a, const void *keys, siz
                                       const uint32_t *idx_c, const void *prepared, size_t points,
                                       const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
                                       uint8_t *ok_out, void *workspace, void *stream);
+/* The same checks with the shares decoded beforehand too: `a_prepared` is
+ * hbrbc_g1_prepare of the count shares (a_i = entry i), so their decoding
+ * and order-r checks run as a launch of their own (e.g. beside
+ * hbrbc_g2_prepare on another stream) and the Miller loops only load them.
+ * Outcomes as hbrbc_pairing_check_prepared_keys. */
+int hbrbc_pairing_check_prepared_pts(const void *a_prepared, const void *keys, size_t key_points,
+                                     const uint32_t *idx_c, const void *prepared, size_t points,
+                                     const uint32_t *idx_b, const uint32_t *idx_d, size_t count,
+                                     uint8_t *ok_out, void *workspace, void *stream);
 /* Per-call shim on host memory (one check, synchronous, current device):
  * *result = 1 if e(a, b) == e(c, d), 0 if not; HBRBC_E_INVALID_ARG for an
  * invalid point. */

@@ -247,6 +247,20 @@ def test_prepared_keys_match_prepared_checks():
     ref = T.pairing_check_prepared(g1, prep, len(cts), ib, idd).cpu().tolist()
     n = len(rows)
     assert got[:n - 3] == ref[:n - 3] and got[n - 3:] == [2, 2, 2]
+    # the shares decoded beforehand too (hbrbc_pairing_check_prepared_pts):
+    # the same outcomes, including invalid shares (off the subgroup,
+    # non-canonical, infinity) decoded into the table
+    bad_shares = [B.g1_bytes(p0), bytes(noncanon), B.g1_bytes(None)]
+    sh = [r[0] for r in rows] + bad_shares
+    ib2 = torch.cat([ib, torch.zeros(3, dtype=torch.int32, device=dev)])
+    idd2 = torch.cat([idd, torch.ones(3, dtype=torch.int32, device=dev)])
+    ic2 = torch.cat([ic, torch.zeros(3, dtype=torch.int32, device=dev)])
+    sprep = T.g1_prepare(_t(sh, 96))
+    pts = T.pairing_check_prepared_pts(sprep, len(sh), ktab, len(keys), ic2, prep, len(cts), ib2,
+                                       idd2).cpu().tolist()
+    ref2 = T.pairing_check_prepared_keys(_t(sh, 96), ktab, len(keys), ic2, prep, len(cts), ib2,
+                                         idd2).cpu().tolist()
+    assert pts == ref2 and pts[:n] == got and pts[n:n + 2] == [2, 2]
     assert ref[n - 1] == 2
     # valid keys: 1 unless tampered; invalid keys (infinity on one side gives 1
     # against a non-1 value, off-subgroup and non-canonical are invalid)

@@ -22,9 +22,12 @@ def main():
             if kern:
                 vals[kern][row["Counter_Name"]].append(float(row["Counter_Value"]))
     per = {}
+    # per call: every kernel's dispatches summed, over the number of calls (one
+    # Miller launch per call; the G1 preparation runs twice per call when the
+    # shares are prepared too -- keys and shares -- with different work)
+    calls = max(1, len(vals.get("miller", {}).get("SQ_INSTS_VALU", [])))
     for kern, cs in vals.items():
-        # the first dispatch of each kernel is the warm-up call; all are equal work
-        per[kern] = {c: sum(v) / len(v) for c, v in cs.items()}
+        per[kern] = {c: sum(v) / calls for c, v in cs.items()}
     stats = {}
     for f in glob.glob(d + "/trace/**/*kernel_stats.csv", recursive=True):
         for row in csv.DictReader(open(f)):
