@@ -118,12 +118,15 @@ class DistExchange:
     (wait() = the current stream / host waits for the exchange, and for gloo
     the copy back to the device), so the pipelined schedule is the same code
     on both.  Every call is counted per collective name: calls and bytes this
-    rank sends (bench line, `exchange.per_rank`)."""
+    rank sends (bench line, `exchange.per_rank`).  `loop`: a one-rank group
+    still issues its collectives (tests/rccl_one_rank.py runs the RCCL calls
+    on the one GPU of a test box); without it a one-rank group copies."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, loop=False):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
+        self.loop = loop
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.backend = dist.get_backend(group)
@@ -143,7 +146,7 @@ class DistExchange:
         async_op returns a handle whose wait() makes the current stream wait."""
         assert out.shape[0] == self.world and inp.shape[0] == self.world
         assert out.is_contiguous() and inp.is_contiguous()
-        if self.world == 1:
+        if self.world == 1 and not self.loop:
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             return None
@@ -162,7 +165,7 @@ class DistExchange:
         """out[s] = inp of rank s (dim 0 of out = ranks, inp flat or not)."""
         assert out.shape[0] == self.world and out.numel() == self.world * inp.numel()
         assert out.is_contiguous() and inp.is_contiguous()
-        if self.world == 1:
+        if self.world == 1 and not self.loop:
             if out.data_ptr() != inp.data_ptr():
                 out.view(-1).copy_(inp.reshape(-1))
             return None

@@ -561,6 +561,48 @@ def test_sharded_two_ranks_gloo_on_one_gpu():
     assert res == {0: "ok", 1: "ok"}, res
 
 
+def test_loop_exchange_issues_one_rank_collectives(tmp_path):
+    """DistExchange(loop=True) on a one-rank group calls the collectives (and
+    counts them) instead of copying; the default copies (CPU, gloo)."""
+    import torch.distributed as dist
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    try:
+        for loop in (False, True):
+            ex = DistExchange(loop=loop)
+            inp = torch.arange(2 * 3 * 5, dtype=torch.uint8).view(1, 6, 5)
+            out = torch.zeros_like(inp)
+            ex.all_to_all(out, inp, name="a2a")
+            assert torch.equal(out, inp)
+            got = torch.zeros((1, 30), dtype=torch.uint8)
+            h = ex.all_gather(got, inp.view(-1), async_op=loop, name="ag")
+            if h is not None:
+                h.wait()
+            assert torch.equal(got.view(-1), inp.view(-1))
+            assert sorted(ex.stats) == (["a2a", "ag"] if loop else [])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_calls():
+    """Every collective call of the multi-GPU bench (Value all-to-all, Echo
+    all-gather, async handles waited on CommTimer's side stream, the state
+    machine's own communicator, the agreement / max-over-ranks all-reduces,
+    all_gather_object, barrier) on a one-rank RCCL group on the box's GPU
+    (tests/rccl_one_rank.py): the RCCL side of the calls the gloo tests run
+    multi-rank."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0",
+               LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1")
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rccl_one_rank.py")
+    r = subprocess.run([sys.executable, "-u", script], env=env, capture_output=True, text=True,
+                       timeout=150)
+    assert r.returncode == 0 and "rccl one-rank: ok" in r.stdout, (r.returncode, r.stdout[-2000:],
+                                                                   r.stderr[-4000:])
+
+
 # ----------------------------------------------------------- HBM footprint --
 BENCH_OBJECTS = [("cfg3", 64, 256 << 10, 8192), ("cfg4", 128, 256 << 10, 4096)]
 
