@@ -1013,7 +1013,8 @@ DEV int decode_g1(const uint8_t *src, Fp &x, Fp &y) {
     return g1_in_subgroup(x, y) ? PT_OK : PT_BAD;      // order r (the crate's into_affine)
 }
 
-DEV int decode_g2(const uint8_t *src, Fp2 &x, Fp2 &y) {
+// the encoding and the curve equation only (no order-r check)
+DEV int decode_g2_curve(const uint8_t *src, Fp2 &x, Fp2 &y) {
     const uint8_t f = src[0];
     if (f & 0xA0) return PT_BAD;
     if (f & 0x40) return all_zero(src, 192, 0x1F) ? PT_INF : PT_BAD;
@@ -1032,7 +1033,12 @@ DEV int decode_g2(const uint8_t *src, Fp2 &x, Fp2 &y) {
     fp_set(bb.c0, kB1);
     bb.c1 = bb.c0;                                     // 4 (u + 1)
     fp2_add(r, r, bb);
-    if (!fp2_eq(l, r)) return PT_BAD;
+    return fp2_eq(l, r) ? PT_OK : PT_BAD;
+}
+
+DEV int decode_g2(const uint8_t *src, Fp2 &x, Fp2 &y) {
+    const int st = decode_g2_curve(src, x, y);
+    if (st != PT_OK) return st;
     return g2_in_subgroup(x, y) ? PT_OK : PT_BAD;
 }
 
@@ -1176,16 +1182,32 @@ DEV void load_line(const uint32_t *src, Fp2 &l0, Fp2 &l1, Fp2 &l4) {
         }
 }
 
-// One lane per G2 point: its 68 lines, and its status (0 ok, 1 infinity,
-// 2 invalid) at pst[q].
+// HB_G2_SPLIT: the point's order-r check and its 68 lines are independent
+// chains (the lines of a point that fails the check are never read: its
+// status says invalid), so they run in two waves side by side -- block 2j
+// checks points 64j.., block 2j + 1 computes their lines (the preparation's
+// latency is the longer chain, not the sum; one ciphertext batch has only
+// 8192 points, an eighth of a wave per SIMD).  0: one lane does both.
+#ifndef HB_G2_SPLIT
+#define HB_G2_SPLIT 1
+#endif
+
+// One lane per G2 point (per role with HB_G2_SPLIT): its 68 lines, and its
+// status (0 ok, 1 infinity, 2 invalid) at pst[q].
 __global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void g2_prepare_kernel(
     const uint8_t *__restrict__ g2, size_t count, uint32_t *__restrict__ prep,
     uint8_t *__restrict__ pst) {
-    const size_t q = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
+    const unsigned blk = HB_G2_SPLIT ? blockIdx.x >> 1 : blockIdx.x;
+    const size_t q = (size_t)blk * kPairBlock + threadIdx.x;
     if (q >= count) return;
     Fp2 xq, yq;
-    const int st = decode_g2(g2 + q * 192, xq, yq);
-    pst[q] = (uint8_t)st;
+    if (HB_G2_SPLIT && !(blockIdx.x & 1)) {   // the status (wave-uniform role)
+        pst[q] = (uint8_t)decode_g2(g2 + q * 192, xq, yq);
+        return;
+    }
+    const int st = HB_G2_SPLIT ? decode_g2_curve(g2 + q * 192, xq, yq)
+                               : decode_g2(g2 + q * 192, xq, yq);
+    if (!HB_G2_SPLIT) pst[q] = (uint8_t)st;
     if (st != PT_OK) return;
     G2Proj T;
     T.x = xq;
@@ -1269,7 +1291,12 @@ DEV void load_g1_key(const uint32_t *src, Fp &x, Fp &y) {
     }
 }
 
-__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_PAIR_WPE, HB_PAIR_WPE))) void g1_prepare_kernel(
+// HB_G1P_WPE: waves per SIMD of the G1 preparation (affine Fp points and
+// their order-r checks need far fewer registers than the tower arithmetic)
+#ifndef HB_G1P_WPE
+#define HB_G1P_WPE HB_PAIR_WPE
+#endif
+__global__ __launch_bounds__(kPairBlock) __attribute__((amdgpu_waves_per_eu(HB_G1P_WPE, HB_G1P_WPE))) void g1_prepare_kernel(
     const uint8_t *__restrict__ g1, size_t count, uint32_t *__restrict__ keys,
     uint8_t *__restrict__ kst) {
     const size_t q = (size_t)blockIdx.x * kPairBlock + threadIdx.x;
@@ -1479,7 +1506,7 @@ size_t pairing_prepared_words(size_t points) { return points * (size_t)kLines * 
 hipError_t launch_g2_prepare(const uint8_t *g2, size_t count, uint32_t *prep, uint8_t *pst,
                              hipStream_t s) {
     if (count == 0) return hipSuccess;
-    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock);
+    const unsigned blocks = (unsigned)((count + kPairBlock - 1) / kPairBlock) * (HB_G2_SPLIT ? 2 : 1);
     hipLaunchKernelGGL(g2_prepare_kernel, dim3(blocks), dim3(kPairBlock), 0, s, g2, count, prep,
                        pst);
     return hipGetLastError();
