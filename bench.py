@@ -1206,10 +1206,18 @@ def run_threshold(args, rank, world, dev):
     # serial chain each): the key shares and the received shares are decoded
     # and checked (order r) on a side stream beside it, and the Miller loops
     # only load them (hbrbc_pairing_check_prepared_pts).  HBRBC_BENCH_F4_SIDE:
-    # 2 (default) keys and shares beside the G2 points, 1 keys only (shares
-    # decoded inside the Miller kernel), 0 everything in order on one stream.
-    mode = int(os.environ.get("HBRBC_BENCH_F4_SIDE", "2"))
+    # 3 (default) the key shares on a stream of their own too (their 256
+    # points are 4 waves, a latency-bound chain like the G2 points'), 2 keys
+    # then shares on one side stream, 1 keys only (shares decoded inside the
+    # Miller kernel), 0 everything in order on one stream; 4 (A/B) the keys
+    # on the main stream before the G2 points; 5 (A/B) the G2 points on a
+    # side stream too and no wait for the previous step (the host runs
+    # ahead: every step's preparations pile up beside the first Miller loop;
+    # +0.8 %, profiles/r6aj_f4_prep_streams_ab.txt).
+    mode = int(os.environ.get("HBRBC_BENCH_F4_SIDE", "3"))
     side = torch.cuda.Stream(dev) if mode > 0 else None
+    kside = torch.cuda.Stream(dev) if mode in (3, 5) else stream if mode == 4 else side
+    gside = torch.cuda.Stream(dev) if mode == 5 else stream
 
     def step():
         if side is None:
@@ -1217,12 +1225,20 @@ def run_threshold(args, rank, world, dev):
             keys = T.g1_prepare(dkeys)
             return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
                                                  ib, idd, ws)
-        side.wait_stream(stream)
-        with torch.cuda.stream(side):
+        if mode != 5:
+            side.wait_stream(stream)
+            kside.wait_stream(stream)
+        with torch.cuda.stream(kside):
             keys = T.g1_prepare(dkeys)
+        with torch.cuda.stream(side):
             sprep = T.g1_prepare(shares) if mode >= 2 else None
-        prep = T.g2_prepare(d2)
+        with torch.cuda.stream(gside):
+            prep = T.g2_prepare(d2)
         stream.wait_stream(side)
+        stream.wait_stream(kside)
+        if gside is not stream:
+            stream.wait_stream(gside)
+            prep.record_stream(stream)
         keys.record_stream(stream)
         if sprep is None:
             return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
