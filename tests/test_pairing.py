@@ -203,6 +203,40 @@ def test_prepared_checks_match_plain_checks():
     assert T.pairing_check_prepared(g1, prep, 3, ib2, idd).cpu().tolist() == [1, 2, 2, 1]
 
 
+def test_g2_prepare_across_blocks():
+    """The G2 preparation checks a point's order (block 2j) and computes its
+    lines (block 2j + 1) in different waves (HB_G2_SPLIT): 130 points, so
+    three block pairs and a ragged last one, with an off-curve, an
+    off-subgroup and an infinity point at the block edges (63, 64, 129) and
+    valid points elsewhere.  Prepared checks give exactly the plain checks'
+    outcomes for every point, against a valid and a tampered G1 side."""
+    import torch
+    from hbbft_amd import threshold as T
+    rng = random.Random(41)
+    base = [B.g2_mul(B.G2_GEN, rng.randrange(1, B.R)) for _ in range(5)]
+    pts = [B.g2_bytes(base[i % 5]) for i in range(130)]
+    bad = bytearray(pts[63])
+    bad[-1] ^= 1                                      # off the curve
+    pts[63] = bytes(bad)
+    _, (q0, _) = _off_subgroup_points()
+    pts[64] = B.g2_bytes(q0)                          # on E', not in the subgroup
+    pts[129] = B.g2_bytes(None)                       # infinity
+    prep = T.g2_prepare(_t(pts, 192))
+    a = B.g1_mul(B.G1_GEN, 5)
+    P, P2 = B.g1_bytes(a), B.g1_bytes(B.g1_add(a, B.G1_GEN))
+    idx = [0, 1, 62, 63, 64, 65, 127, 128, 129]
+    # odd checks e(P, Q_k) == e(P, Q_k); even ones e(P, Q_k) == e(P + G, Q_(k+1))
+    dix = [k if n % 2 else (k + 1) % 130 for n, k in enumerate(idx)]
+    g1 = _t([x for n, k in enumerate(idx) for x in (P, P if n % 2 else P2)], 96)
+    dev = "cuda:0"
+    ib = torch.tensor(idx, dtype=torch.int32, device=dev)
+    idd = torch.tensor(dix, dtype=torch.int32, device=dev)
+    got = T.pairing_check_prepared(g1, prep, len(pts), ib, idd).cpu().tolist()
+    g2 = _t([x for k, d in zip(idx, dix) for x in (pts[k], pts[d])], 192)
+    ref = T.pairing_check_batch(g1, g2).cpu().tolist()
+    assert got == ref == [0, 1, 2, 2, 2, 1, 0, 1, 0]
+
+
 def test_prepared_keys_match_prepared_checks():
     """Checks against a table of prepared G1 keys (hbbft's pk_i, decoded and
     checked once) give exactly the outcomes of the same checks with both G1
