@@ -1213,33 +1213,44 @@ def run_threshold(args, rank, world, dev):
     # on the main stream before the G2 points; 5 (A/B) the G2 points on a
     # side stream too and no wait for the previous step (the host runs
     # ahead: every step's preparations pile up beside the first Miller loop;
-    # +0.8 %, profiles/r6aj_f4_prep_streams_ab.txt).
+    # +0.8 %, profiles/r6aj_f4_prep_streams_ab.txt); 6 (A/B) as 3 with the
+    # G2 points on a side stream, and step i + 1's preparations enqueued
+    # when step i's Miller loop is, so they run beside it and no further
+    # (-3.5 %: the Miller kernel's two residency rounds become three).
     mode = int(os.environ.get("HBRBC_BENCH_F4_SIDE", "3"))
     side = torch.cuda.Stream(dev) if mode > 0 else None
-    kside = torch.cuda.Stream(dev) if mode in (3, 5) else stream if mode == 4 else side
-    gside = torch.cuda.Stream(dev) if mode == 5 else stream
+    kside = torch.cuda.Stream(dev) if mode in (3, 5, 6) else stream if mode == 4 else side
+    gside = torch.cuda.Stream(dev) if mode in (5, 6) else stream
+    pending = []
 
-    def step():
-        if side is None:
-            prep = T.g2_prepare(d2)
-            keys = T.g1_prepare(dkeys)
-            return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
-                                                 ib, idd, ws)
-        if mode != 5:
+    def prepare():
+        if mode != 5:   # from this point of the main stream on
             side.wait_stream(stream)
             kside.wait_stream(stream)
+            gside.wait_stream(stream)
         with torch.cuda.stream(kside):
             keys = T.g1_prepare(dkeys)
         with torch.cuda.stream(side):
             sprep = T.g1_prepare(shares) if mode >= 2 else None
         with torch.cuda.stream(gside):
             prep = T.g2_prepare(d2)
+        return keys, sprep, prep
+
+    def step(prefetch=False):
+        if side is None:
+            prep = T.g2_prepare(d2)
+            keys = T.g1_prepare(dkeys)
+            return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
+                                                 ib, idd, ws)
+        keys, sprep, prep = pending.pop() if pending else prepare()
         stream.wait_stream(side)
         stream.wait_stream(kside)
         if gside is not stream:
             stream.wait_stream(gside)
             prep.record_stream(stream)
         keys.record_stream(stream)
+        if prefetch:   # the next step's, beside this step's Miller loop
+            pending.append(prepare())
         if sprep is None:
             return T.pairing_check_prepared_keys(shares, keys, dkeys.shape[0], dic, prep, 2 * ng,
                                                  ib, idd, ws)
@@ -1257,8 +1268,8 @@ def run_threshold(args, rank, world, dev):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.f4_steps):
-        step()
+    for j in range(args.f4_steps):
+        step(prefetch=mode == 6 and j + 1 < args.f4_steps)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
