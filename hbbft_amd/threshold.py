@@ -185,9 +185,10 @@ def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
     ThresholdDecrypt receives them: ciphertexts = [(hash G2, W G2)], shares =
     [(ciphertext index, share G1, pk_share G1)].  Each ciphertext's H and W
     are prepared once, each distinct key share pk_i is decoded and checked
-    once (the crate holds the validator set's key shares as points); shares
-    are grouped by ciphertext so a wave shares its lines.  Returns bools in
-    the order of `shares`."""
+    once (the crate holds the validator set's key shares as points), the
+    received shares are decoded in a launch of their own; shares are grouped
+    by ciphertext so a wave shares its lines.  Returns bools in the order of
+    `shares`."""
     import numpy as np
     torch = _torch()
     if not shares:
@@ -197,12 +198,10 @@ def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
     for j, (h, w) in enumerate(ciphertexts):
         g2[2 * j] = np.frombuffer(h, np.uint8)
         g2[2 * j + 1] = np.frombuffer(w, np.uint8)
-    prep = g2_prepare(torch.from_numpy(g2).to(dev))
     key_ids = {}
     for _, _, pk in shares:
         key_ids.setdefault(bytes(pk), len(key_ids))
     kt = np.stack([np.frombuffer(k, np.uint8) for k in key_ids])
-    ktab = g1_prepare(torch.from_numpy(kt).to(dev))
     order = sorted(range(len(shares)), key=lambda i: shares[i][0])
     g1 = np.empty((len(shares), G1_BYTES), np.uint8)
     ib = np.empty(len(shares), np.int32)
@@ -212,9 +211,29 @@ def verify_decryption_shares_grouped(ciphertexts, shares, device=0):
         g1[r] = np.frombuffer(share, np.uint8)
         ib[r] = 2 * ct
         ic[r] = key_ids[bytes(pk)]
-    ok = pairing_check_prepared_keys(torch.from_numpy(g1).to(dev), ktab, len(key_ids),
-                                     torch.from_numpy(ic).to(dev), prep, 2 * len(ciphertexts),
-                                     torch.from_numpy(ib).to(dev), torch.from_numpy(ib + 1).to(dev))
+    d2, dk, d1 = (torch.from_numpy(x).to(dev) for x in (g2, kt, g1))
+    # the three preparations are independent: the G2 points and the key
+    # shares are latency-bound chains on few waves, the received shares fill
+    # the chip -- each on a stream of its own, the checks wait for all three
+    cur = torch.cuda.current_stream(dev)
+    sides = [torch.cuda.Stream(dev) for _ in range(3)]
+    for s_ in sides:
+        s_.wait_stream(cur)
+    with torch.cuda.stream(sides[0]):
+        prep = g2_prepare(d2)
+    with torch.cuda.stream(sides[1]):
+        ktab = g1_prepare(dk)
+    with torch.cuda.stream(sides[2]):
+        sprep = g1_prepare(d1)
+    for s_ in sides:
+        cur.wait_stream(s_)
+    for t_, s_ in ((d2, sides[0]), (dk, sides[1]), (d1, sides[2])):
+        t_.record_stream(s_)
+    for t_ in (prep, ktab, sprep):
+        t_.record_stream(cur)
+    ok = pairing_check_prepared_pts(sprep, len(shares), ktab, len(key_ids),
+                                    torch.from_numpy(ic).to(dev), prep, 2 * len(ciphertexts),
+                                    torch.from_numpy(ib).to(dev), torch.from_numpy(ib + 1).to(dev))
     okh = ok.cpu().tolist()
     out = [False] * len(shares)
     for r, i in enumerate(order):
